@@ -1,0 +1,191 @@
+/* pggan_hip.h — C ABI of libpggan_hip.so, the gfx950 (MI355X) kernels of the
+ * PGGAN G+D+R1 training step.
+ *
+ * The reference (yukyeongleee/pggan) has no native FFI on this path: its ops are
+ * torch.nn.Conv2d / nn.Linear inside ConstrainedLayer (lib/layers.py:28-108)
+ * and autograd supplies backward and the R1 double-backward
+ * (lib/loss.py:125-135).  Each entry point below replaces one reference op (or a
+ * fused group of them) and names the reference lines it stands in for.  A
+ * maintainer binds these with ctypes.
+ *
+ * Conventions
+ *  - every function returns 0 (PG_OK) or a negative error code; the message is
+ *    available from pg_last_error();
+ *  - all pointers are DEVICE pointers owned by the caller; the library never
+ *    allocates; `stream` is a hipStream_t passed as void* (0 = null stream);
+ *  - dtype: PG_F32 (exact-fp32 parity mode) or PG_BF16 (bf16 storage, fp32
+ *    accumulation); weights/biases/gradients/optimizer state are always fp32;
+ *  - activations are NHWC with an explicit channel stride `*_cs` (elements);
+ *    images at the API boundary are NCHW fp32 like the reference;
+ *  - kernels are stateless and re-entrant; outputs are written fully unless an
+ *    ACCUM flag / "accumulates" note says the result is added.
+ */
+#ifndef PGGAN_HIP_H
+#define PGGAN_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_OK 0
+#define PG_ERR_ARG (-1)
+#define PG_ERR_HIP (-2)
+#define PG_ERR_UNSUPPORTED (-3)
+
+#define PG_F32 0
+#define PG_BF16 1
+
+const char* pg_last_error(void);
+int pg_version(void);
+
+/* ---- equalized-LR 3x3 convolution (lib/layers.py:66-89, ConstrainedLayer.forward :58-63)
+ * y = out_scale * post(conv3x3(pre(x), wpk) + bias)
+ * wpk: packed weights from pg_conv3x3_pack with the He constant folded in.
+ * The same kernel runs the forward pass, the input-gradient pass (dgrad, with
+ * PG_PACK_DGRAD weights) and the R1 tangent pass (no bias, PG_CONV_MASK). */
+#define PG_CONV_UPS_IN 1  /* x is H/2 x W/2; nearest x2 upsample on load (lib/utils.py:106-118) */
+#define PG_CONV_BIAS 2    /* + bias[cout] (fp32, He constant folded) */
+#define PG_CONV_LRELU 4   /* leaky relu(slope) on the conv result */
+#define PG_CONV_MASK 8    /* multiply by lrelu'(aux) (aux at output resolution, channel stride aux_cs) */
+#define PG_CONV_POOL 16   /* 2x2 pool of the activated result (avg: out_scale=0.25, sum: 1.0) */
+#define PG_CONV_ACCUM 32  /* y += result */
+
+typedef struct {
+  int B, H, W;     /* conv output spatial size (after the optional input upsample) */
+  int cin, cout;   /* channels as packed (cin: multiple of 8, <=16 or multiple of 32) */
+  int x_cs, y_cs, aux_cs, y2_cs; /* channel strides (elements) of x, y, aux, y2 */
+  int flags;
+  float slope;     /* leaky relu slope */
+  float out_scale;
+} pg_conv_desc;
+
+#define PG_PACK_FWD 0    /* wpk[cout_p][9][cin_p]   = scale * W[o][c][tap]          */
+#define PG_PACK_DGRAD 1  /* wpk[cin_p16][9][cout_p] = scale * W[o][c][8 - tap]      */
+size_t pg_conv3x3_packed_elems(int mode, int cout, int cin);
+int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw, float scale,
+                    void* wpk, void* stream);
+int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                   const float* bias, const void* aux, void* y, void* y2, void* stream);
+/* weight gradient, accumulates: dw[o][c][ky][kx] += scale * sum_p gz[p][o] * x[p+tap][c]
+ * (desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold PG_CONV_UPS_IN) */
+int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
+                     float* dw, void* stream);
+/* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
+int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
+                 void* stream);
+
+/* ---- PixelwiseVectorNorm (lib/layers.py:8-14) over the channel axis of NHWC */
+int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, void* stream);
+/* gz = PN^T(gy) * lrelu'(u), u = the PN input (a leaky-relu output) (lib/blocks.py:128-139) */
+int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, const void* gy,
+                         float slope, int apply_mask, void* gz, void* stream);
+
+/* ---- elementwise helpers (NHWC, channel stride cs) */
+/* out[p] = scale * g[ups ? p/2 : p] * (y ? lrelu'(y[p]) : 1)   (avg-pool backward, lib/blocks.py:193) */
+int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
+                   const void* y, float scale, float slope, int ups, int out_cs, void* out,
+                   void* stream);
+/* 2x2 average pool (lib/utils.py:120-124), input B x H x W */
+int pg_avgpool2(int dtype, int B, int H, int W, int C, int x_cs, const void* x, int y_cs, void* y,
+                void* stream);
+/* out = a*x + b*y over n elements (fade-in blends, pggan/nets.py:155-156, 263-265) */
+int pg_blend(int dtype, size_t n, float a, const void* x, float b, const void* y, void* out,
+             void* stream);
+
+/* ---- RGB layers (toRGBBlock lib/blocks.py:153-170, fromRGBBlock :271-292) */
+/* G output image (NCHW fp32): img = alpha*toRGB_s(x) + (1-alpha)*up2(toRGB_{s-1}(xp));
+ * xp == NULL -> img = toRGB_s(x) (stage 0).  w: [3][C] fp32 raw, b: [3], c: He constant. */
+int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
+               const float* b, float c, int Cp, int xp_cs, const void* xp, const float* wp,
+               const float* bp, float cp, float alpha, float* img, void* stream);
+/* backward of pg_rgb_out: writes gx (NHWC, T) and gxp; accumulates dw/db/dwp/dbp */
+int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
+                   float c, int Cp, int xp_cs, const void* xp, const float* wp, float cp,
+                   float alpha, const float* gimg, void* gx, void* gxp, float* dw, float* db,
+                   float* dwp, float* dbp, void* stream);
+/* fromRGB: y = lrelu(c*(W . img_in + b)), img_in = down ? avgpool2(img) : img  (img NCHW fp32);
+ * R = output resolution.  b == NULL -> no bias; mask_y != NULL -> tangent mode:
+ * y = c*(W . img_in) * lrelu'(mask_y) (no activation) */
+int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
+                void* stream);
+/* backward: gimg[b][i][p] += c * sum_o gz[p(/2)][o] W[o][i] * (down ? 0.25 : 1) (if gimg);
+ * dw[o][i] += c sum gz*img_in, db[o] += c sum gz (if dw/db) */
+int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                    float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
+                    void* stream);
+/* real-image fade (pggan/model.py:217-221): out = (1-a)*up2(avgpool2(x)) + a*x, NCHW fp32 */
+int pg_img_fade(int B, int C, int R, const float* x, float alpha, float* out, void* stream);
+
+/* ---- equalized linear (lib/layers.py:92-108)
+ * x: [B][K] (or NHWC [B][16][C] when PG_LIN_IN_CHW: k = c*16 + hw, the reference's NCHW flatten)
+ * y: [B][N] (or NHWC [B][16][N/16] when PG_LIN_OUT_CHW: n = c*16 + hw, pggan/nets.py:130) */
+#define PG_LIN_BIAS 1
+#define PG_LIN_LRELU 2
+#define PG_LIN_MASK 4     /* multiply by lrelu'(aux), aux laid out like y */
+#define PG_LIN_IN_CHW 8
+#define PG_LIN_OUT_CHW 16
+#define PG_LIN_F32_IN 32  /* x is fp32 regardless of dtype */
+#define PG_LIN_F32_OUT 64 /* y is fp32 regardless of dtype */
+typedef struct {
+  int B, K, N;
+  int in_cs, out_cs;  /* channel strides for the CHW-mapped sides */
+  int flags;
+  float scale, slope;
+} pg_linear_desc;
+int pg_linear_fwd(int dtype, const pg_linear_desc* d, const void* x, const float* w,
+                  const float* b, const void* aux, void* y, void* stream);
+/* gx[b][k] = scale * sum_n gy[b][n] W[n][k]  (* lrelu'(aux[b][k]) if PG_LIN_MASK); flags
+ * IN_CHW/F32_IN describe gx, OUT_CHW/F32_OUT describe gy */
+int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
+                    const void* aux, void* gx, void* stream);
+/* accumulates dw[n][k] += scale sum_b gy[b][n] x[b][k]; db[n] += scale sum_b gy[b][n] */
+int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const void* gy, float* dw,
+                    float* db, void* stream);
+
+/* ---- minibatch stddev (lib/blocks.py:204-233), x: [B][HW][C] (cs x_cs) -> y: [B][HW][y_cs]
+ * (channel C = group stddev, channels C+1..y_cs-1 = 0) */
+int pg_mbstd_fwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y_cs, void* y,
+                 void* stream);
+/* gx = gy[:, :C] + d mbstd/dx ^T gy[:, C] */
+int pg_mbstd_bwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y_cs,
+                 const void* gy, void* gx, void* stream);
+/* R1 second-order pieces at mbstd: tangent output tout = [a, sdot, 0..] and the injection
+ * inj = d/dx <a, J^T gy> (added into the second backward), a = tangent at the input */
+int pg_mbstd_r1(int dtype, int B, int HW, int C, int x_cs, const void* x, const void* a,
+                int y_cs, const void* gy, void* tout, void* inj, void* stream);
+
+/* ---- losses (lib/loss.py:119-135, pggan/loss.py:5-27); all fp32, device-resident scalars
+ * logits [B]: loss = mean softplus(target ? -l : l); u = dloss/dl (scaled by w);
+ * h = d u / d l (for the R1 double-backward).  loss_out[0] += w * loss. */
+int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out, float* u,
+                float* h, void* stream);
+/* R1 = 0.5 * mean_b sum g^2 accumulated into r1_out[0]; gbar = g / B  (g: [n] fp32, B samples) */
+int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream);
+/* WGAN-GP optional mode (pggan/loss.py:54-92): interp = eps*xr + (1-eps)*xf (per-sample eps) */
+int pg_gp_interp(int B, size_t per, const float* xr, const float* xf, const float* eps,
+                 float* out, void* stream);
+/* gp = w * sum_b (||g_b|| - 1)^2 -> gp_out[0] (accumulate); gbar_b = w*2*(||g_b||-1)/||g_b|| g_b;
+ * norms[B] workspace */
+int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, float* norms,
+                  float* gbar, void* stream);
+
+/* out = x + y*z (fp32; the R1 logit injection u + h*t, pggan/loss.py:16-27) */
+int pg_mul_add(size_t n, const float* x, const float* y, const float* z, float* out, void* stream);
+
+/* ---- Adam (torch.optim.Adam, lib/model.py:95-97; single-tensor update order) over one flat
+ * fp32 range (the live parameters of a net are kept contiguous; dead ones are not passed) */
+int pg_adam(size_t n, float* p, const float* g, float* m, float* v, float lr, float beta1,
+            float beta2, float eps, int step, void* stream);
+
+/* ---- N(0,1) latents (counter-based, deterministic in (seed, offset)) */
+int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream);
+/* dtype conversion helpers */
+int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

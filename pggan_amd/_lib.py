@@ -1,0 +1,313 @@
+"""ctypes binding of libpggan_hip.so (the C ABI declared in include/pggan_hip.h).
+
+`HipOps` is the tensor-level op set the step engine is written against: every
+method takes torch tensors resident on the GPU, passes raw device pointers and
+the current HIP stream to one C-ABI entry point, and raises RuntimeError on a
+non-zero status.  There is no fallback: if the shared library is missing or a
+tensor is not on the GPU the call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+PG_F32, PG_BF16 = 0, 1
+
+CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
+PACK_FWD, PACK_DGRAD = 0, 1
+LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
+    1, 2, 4, 8, 16, 32, 64)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpggan_hip.so")
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in
+                ("B", "H", "W", "cin", "cout", "x_cs", "y_cs", "aux_cs", "y2_cs", "flags")] + \
+               [("slope", ctypes.c_float), ("out_scale", ctypes.c_float)]
+
+
+class LinearDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("B", "K", "N", "in_cs", "out_cs", "flags")] + \
+               [("scale", ctypes.c_float), ("slope", ctypes.c_float)]
+
+
+_lib = None
+
+_VP, _I, _F, _SZ, _U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64
+_SIGS = {
+    "pg_version": ([], _I),
+    "pg_conv3x3_packed_elems": ([_I, _I, _I], _SZ),
+    "pg_conv3x3_pack": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP], _I),
+    "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
+    "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
+    "pg_unpool_mask": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _F, _F, _I, _I, _VP, _VP], _I),
+    "pg_avgpool2": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _VP], _I),
+    "pg_blend": ([_I, _SZ, _F, _VP, _F, _VP, _VP, _VP], _I),
+    "pg_rgb_out": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _I, _I, _VP, _VP, _VP, _F, _F, _VP,
+                    _VP], _I),
+    "pg_rgb_out_bwd": ([_I, _I, _I, _I, _I, _VP, _VP, _F, _I, _I, _VP, _VP, _F, _F, _VP, _VP,
+                        _VP, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_from_rgb": ([_I, _I, _I, _I, _VP, _I, _VP, _VP, _F, _F, _VP, _I, _VP, _VP], _I),
+    "pg_from_rgb_bwd": ([_I, _I, _I, _I, _VP, _I, _VP, _F, _I, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_img_fade": ([_I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_linear_fwd": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_linear_dgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_linear_wgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_mbstd_fwd": ([_I, _I, _I, _I, _I, _VP, _I, _VP, _VP], _I),
+    "pg_mbstd_bwd": ([_I, _I, _I, _I, _I, _VP, _I, _VP, _VP, _VP], _I),
+    "pg_mbstd_r1": ([_I, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP], _I),
+    "pg_bce_loss": ([_I, _VP, _I, _F, _VP, _VP, _VP, _VP], _I),
+    "pg_r1_penalty": ([_I, _SZ, _VP, _VP, _VP, _VP], _I),
+    "pg_gp_interp": ([_I, _SZ, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_gp_penalty": ([_I, _SZ, _VP, _F, _VP, _VP, _VP, _VP], _I),
+    "pg_mul_add": ([_SZ, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_adam": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _F, _I, _VP], _I),
+    "pg_randn": ([_SZ, _U64, _U64, _VP, _VP], _I),
+    "pg_cast": ([_I, _I, _SZ, _VP, _VP, _VP], _I),
+}
+SYMBOLS = ["pg_last_error"] + list(_SIGS)
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libpggan_hip.so and declare every signature.  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"pggan_amd: HIP library not built: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    lib.pg_last_error.argtypes = []
+    lib.pg_last_error.restype = ctypes.c_char_p
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _p(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class HipOps:
+    """Tensor-level wrappers of the C ABI.  `dtype` = storage dtype of activations."""
+
+    def __init__(self, dtype: torch.dtype = torch.float32):
+        self.lib = load_library()
+        assert dtype in (torch.float32, torch.bfloat16)
+        self.tdtype = dtype
+        self.dt = PG_F32 if dtype == torch.float32 else PG_BF16
+
+    # -- plumbing --------------------------------------------------------
+    def _s(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.pg_last_error().decode(errors="replace")
+            raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+    def _cuda(self, *ts):
+        for t in ts:
+            if t is not None and not t.is_cuda:
+                raise RuntimeError("pggan_amd: HIP op called with a CPU tensor (no CPU fallback)")
+
+    def _dt(self, t):
+        return PG_F32 if t.dtype == torch.float32 else PG_BF16
+
+    # -- conv ------------------------------------------------------------
+    def packed_elems(self, mode, cout, cin):
+        return int(self.lib.pg_conv3x3_packed_elems(mode, cout, cin))
+
+    def conv_pack(self, mode, w, scale, out):
+        self._cuda(w, out)
+        cout, cin = w.shape[0], w.shape[1]
+        self._chk(self.lib.pg_conv3x3_pack(self._dt(out), mode, cout, cin, _p(w), scale, _p(out),
+                                           self._s()), "conv3x3_pack")
+
+    def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
+                bias=None, aux=None, y2=None):
+        self._cuda(x, wpk, y, bias, aux, y2)
+        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], y.shape[-1],
+                     aux.shape[-1] if aux is not None else 0,
+                     y2.shape[-1] if y2 is not None else 0, flags, slope, out_scale)
+        self._chk(self.lib.pg_conv3x3_fwd(self._dt(y), ctypes.byref(d), _p(x), _p(wpk), _p(bias),
+                                          _p(aux), _p(y), _p(y2), self._s()), "conv3x3_fwd")
+
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale):
+        self._cuda(x, gz, dw)
+        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0,
+                     CONV_UPS_IN if ups else 0, 0.0, 1.0)
+        self._chk(self.lib.pg_conv3x3_wgrad(self._dt(gz), ctypes.byref(d), _p(x), _p(gz), scale,
+                                            _p(dw), self._s()), "conv3x3_wgrad")
+
+    def bias_grad(self, g, db, C, scale):
+        self._cuda(g, db)
+        npix = g.numel() // g.shape[-1]
+        self._chk(self.lib.pg_bias_grad(self._dt(g), npix, C, g.shape[-1], _p(g), scale, _p(db),
+                                        self._s()), "bias_grad")
+
+    # -- pixel norm ------------------------------------------------------
+    def pixnorm(self, x, y, C):
+        self._cuda(x, y)
+        npix = x.numel() // x.shape[-1]
+        self._chk(self.lib.pg_pixnorm_fwd(self._dt(x), npix, C, x.shape[-1], _p(x), _p(y),
+                                          self._s()), "pixnorm_fwd")
+
+    def pixnorm_lrelu_bwd(self, u, gy, gz, C, slope, mask=True):
+        self._cuda(u, gy, gz)
+        npix = u.numel() // u.shape[-1]
+        self._chk(self.lib.pg_pixnorm_lrelu_bwd(self._dt(u), npix, C, u.shape[-1], _p(u), _p(gy),
+                                                slope, 1 if mask else 0, _p(gz), self._s()),
+                  "pixnorm_lrelu_bwd")
+
+    # -- elementwise -------------------------------------------------------
+    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):
+        self._cuda(g, y, out)
+        self._chk(self.lib.pg_unpool_mask(self._dt(out), B, H, W, C, g.shape[-1], _p(g),
+                                          y.shape[-1] if y is not None else 0, _p(y), scale, slope,
+                                          1 if ups else 0, out.shape[-1], _p(out), self._s()),
+                  "unpool_mask")
+
+    def avgpool2(self, x, y, *, B, H, W, C):
+        self._cuda(x, y)
+        self._chk(self.lib.pg_avgpool2(self._dt(x), B, H, W, C, x.shape[-1], _p(x), y.shape[-1],
+                                       _p(y), self._s()), "avgpool2")
+
+    def blend(self, a, x, b, y, out):
+        self._cuda(x, y, out)
+        self._chk(self.lib.pg_blend(self._dt(out), out.numel(), a, _p(x), b, _p(y), _p(out),
+                                    self._s()), "blend")
+
+    # -- RGB ---------------------------------------------------------------
+    def rgb_out(self, x, w, b, c, img, *, B, R, C, xp=None, wp=None, bp=None, cp=0.0, Cp=0,
+                alpha=1.0):
+        self._cuda(x, w, b, img, xp, wp, bp)
+        self._chk(self.lib.pg_rgb_out(self._dt(x), B, R, C, x.shape[-1], _p(x), _p(w), _p(b), c, Cp,
+                                      xp.shape[-1] if xp is not None else 0, _p(xp), _p(wp), _p(bp),
+                                      cp, alpha, _p(img), self._s()), "rgb_out")
+
+    def rgb_out_bwd(self, x, w, c, gimg, gx, dw, db, *, B, R, C, xp=None, wp=None, cp=0.0, Cp=0,
+                    alpha=1.0, gxp=None, dwp=None, dbp=None):
+        self._cuda(x, w, gimg, gx, dw, db, xp, wp, gxp, dwp, dbp)
+        self._chk(self.lib.pg_rgb_out_bwd(self._dt(x), B, R, C, x.shape[-1], _p(x), _p(w), c, Cp,
+                                          xp.shape[-1] if xp is not None else 0, _p(xp), _p(wp), cp,
+                                          alpha, _p(gimg), _p(gx), _p(gxp), _p(dw), _p(db), _p(dwp),
+                                          _p(dbp), self._s()), "rgb_out_bwd")
+
+    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
+        self._cuda(img, w, b, y, mask_y)
+        self._chk(self.lib.pg_from_rgb(self._dt(y), B, R, C, _p(img), 1 if down else 0, _p(w), _p(b),
+                                       c, slope, _p(mask_y), y.shape[-1], _p(y), self._s()),
+                  "from_rgb")
+
+    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None):
+        self._cuda(gz, w, img, gimg, dw, db)
+        self._chk(self.lib.pg_from_rgb_bwd(self._dt(gz), B, R, C, _p(img), 1 if down else 0, _p(w),
+                                           c, gz.shape[-1], _p(gz), _p(gimg), _p(dw), _p(db),
+                                           self._s()), "from_rgb_bwd")
+
+    def img_fade(self, x, alpha, out):
+        self._cuda(x, out)
+        B, C, R, _ = x.shape
+        self._chk(self.lib.pg_img_fade(B, C, R, _p(x), alpha, _p(out), self._s()), "img_fade")
+
+    # -- linear ------------------------------------------------------------
+    def _lin(self, B, K, N, flags, scale, slope, x_t, y_t):
+        in_cs = x_t.shape[-1] if (flags & LIN_IN_CHW) else 0
+        out_cs = y_t.shape[-1] if (flags & LIN_OUT_CHW) else 0
+        if x_t.dtype == torch.float32 and self.dt != PG_F32:
+            flags |= LIN_F32_IN
+        if y_t.dtype == torch.float32 and self.dt != PG_F32:
+            flags |= LIN_F32_OUT
+        return LinearDesc(B, K, N, in_cs, out_cs, flags, scale, slope)
+
+    def linear(self, x, w, b, y, *, B, flags, scale, slope=0.2, aux=None):
+        self._cuda(x, w, b, y, aux)
+        N, K = w.shape
+        d = self._lin(B, K, N, flags, scale, slope, x, y)
+        self._chk(self.lib.pg_linear_fwd(self.dt, ctypes.byref(d), _p(x), _p(w), _p(b), _p(aux),
+                                         _p(y), self._s()), "linear_fwd")
+
+    def linear_dgrad(self, gy, w, gx, *, B, flags, scale, slope=0.2, aux=None):
+        self._cuda(gy, w, gx, aux)
+        N, K = w.shape
+        d = self._lin(B, K, N, flags, scale, slope, gx, gy)
+        self._chk(self.lib.pg_linear_dgrad(self.dt, ctypes.byref(d), _p(gy), _p(w), _p(aux), _p(gx),
+                                           self._s()), "linear_dgrad")
+
+    def linear_wgrad(self, x, gy, dw, db, *, B, flags, scale):
+        self._cuda(x, gy, dw, db)
+        N, K = dw.shape
+        d = self._lin(B, K, N, flags, scale, 0.0, x, gy)
+        self._chk(self.lib.pg_linear_wgrad(self.dt, ctypes.byref(d), _p(x), _p(gy), _p(dw), _p(db),
+                                           self._s()), "linear_wgrad")
+
+    # -- minibatch stddev ----------------------------------------------------
+    def mbstd_fwd(self, x, y, *, B, HW, C):
+        self._cuda(x, y)
+        self._chk(self.lib.pg_mbstd_fwd(self._dt(x), B, HW, C, x.shape[-1], _p(x), y.shape[-1],
+                                        _p(y), self._s()), "mbstd_fwd")
+
+    def mbstd_bwd(self, x, gy, gx, *, B, HW, C):
+        self._cuda(x, gy, gx)
+        self._chk(self.lib.pg_mbstd_bwd(self._dt(x), B, HW, C, x.shape[-1], _p(x), gy.shape[-1],
+                                        _p(gy), _p(gx), self._s()), "mbstd_bwd")
+
+    def mbstd_r1(self, x, a, gy, tout, inj, *, B, HW, C):
+        self._cuda(x, a, gy, tout, inj)
+        self._chk(self.lib.pg_mbstd_r1(self._dt(x), B, HW, C, x.shape[-1], _p(x), _p(a),
+                                       gy.shape[-1], _p(gy), _p(tout), _p(inj), self._s()),
+                  "mbstd_r1")
+
+    # -- losses / optimizer / rng ------------------------------------------
+    def bce(self, logits, target, w, loss, u, h):
+        self._cuda(logits, loss, u, h)
+        self._chk(self.lib.pg_bce_loss(logits.numel(), _p(logits), 1 if target else 0, w, _p(loss),
+                                       _p(u), _p(h), self._s()), "bce_loss")
+
+    def r1_penalty(self, g, B, r1, gbar):
+        self._cuda(g, r1, gbar)
+        self._chk(self.lib.pg_r1_penalty(B, g.numel(), _p(g), _p(r1), _p(gbar), self._s()),
+                  "r1_penalty")
+
+    def gp_interp(self, xr, xf, eps, out):
+        self._cuda(xr, xf, eps, out)
+        B = xr.shape[0]
+        self._chk(self.lib.pg_gp_interp(B, xr.numel() // B, _p(xr), _p(xf), _p(eps), _p(out),
+                                        self._s()), "gp_interp")
+
+    def gp_penalty(self, g, w, gp, norms, gbar):
+        self._cuda(g, gp, norms, gbar)
+        B = g.shape[0]
+        self._chk(self.lib.pg_gp_penalty(B, g.numel() // B, _p(g), w, _p(gp), _p(norms), _p(gbar),
+                                         self._s()), "gp_penalty")
+
+    def mul_add(self, x, y, z, out):
+        self._cuda(x, y, z, out)
+        self._chk(self.lib.pg_mul_add(out.numel(), _p(x), _p(y), _p(z), _p(out), self._s()),
+                  "mul_add")
+
+    def adam(self, p, g, m, v, *, lr, beta1, beta2, eps, step):
+        self._cuda(p, g, m, v)
+        self._chk(self.lib.pg_adam(p.numel(), _p(p), _p(g), _p(m), _p(v), lr, beta1, beta2, eps,
+                                   step, self._s()), "adam")
+
+    def randn(self, out, seed, offset):
+        self._cuda(out)
+        self._chk(self.lib.pg_randn(out.numel(), seed, offset, _p(out), self._s()), "randn")
+
+    def cast(self, x, y):
+        self._cuda(x, y)
+        self._chk(self.lib.pg_cast(self._dt(x), self._dt(y), x.numel(), _p(x), _p(y), self._s()),
+                  "cast")

@@ -1,0 +1,103 @@
+// Shared device helpers for the PGGAN gfx950 kernels.
+//
+// Storage dtypes: DT_F32 (parity mode) and DT_BF16 (perf mode, fp32 accumulate).
+// Activations are NHWC with a channel stride (`cs`) that may exceed the logical
+// channel count (the mbstd output is padded 513 -> 544 so the following conv
+// sees a multiple of 32 input channels).  Images are NCHW fp32 (the reference's
+// tensor layout at the API boundary).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pggan_hip.h"
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+#define PG_WAVE 64
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// round-to-nearest-even; NaN stays NaN
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct Ty;
+template <> struct Ty<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+  // 4 consecutive elements
+  static __device__ __forceinline__ void ld4(const float* p, float v[4]) {
+    f32x4_t q = *reinterpret_cast<const f32x4_t*>(p);
+    v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+  }
+  static __device__ __forceinline__ void st4(float* p, const float v[4]) {
+    f32x4_t q = {v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4_t*>(p) = q;
+  }
+};
+template <> struct Ty<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+  static __device__ __forceinline__ void ld4(const bf16_t* p, float v[4]) {
+    u32x2_t q = *reinterpret_cast<const u32x2_t*>(p);
+    v[0] = __uint_as_float(q[0] << 16); v[1] = __uint_as_float(q[0] & 0xffff0000u);
+    v[2] = __uint_as_float(q[1] << 16); v[3] = __uint_as_float(q[1] & 0xffff0000u);
+  }
+  static __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
+    u32x2_t q;
+    q[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    q[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<u32x2_t*>(p) = q;
+  }
+};
+
+__device__ __forceinline__ float lrelu_f(float v, float slope) { return v > 0.f ? v : v * slope; }
+__device__ __forceinline__ float lmask_f(float y, float slope) { return y > 0.f ? 1.f : slope; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum; `red` must hold >= blockDim.x/64 floats; result valid in all threads
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// ---- error plumbing -------------------------------------------------------
+void pg_set_error(const char* fmt, ...);
+
+#define PG_CHECK_ARG(cond, ...)             \
+  do {                                      \
+    if (!(cond)) {                          \
+      pg_set_error(__VA_ARGS__);            \
+      return PG_ERR_ARG;                    \
+    }                                       \
+  } while (0)
+
+#define PG_LAUNCH_CHECK()                                                       \
+  do {                                                                          \
+    hipError_t e_ = hipGetLastError();                                          \
+    if (e_ != hipSuccess) {                                                     \
+      pg_set_error("%s: HIP launch error: %s", __func__, hipGetErrorString(e_)); \
+      return PG_ERR_HIP;                                                        \
+    }                                                                           \
+  } while (0)
+
+static inline int pg_cdiv(int a, int b) { return (a + b - 1) / b; }

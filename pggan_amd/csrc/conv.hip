@@ -1,0 +1,585 @@
+// Equalized-LR 3x3 convolution on gfx950 MFMA: forward / dgrad / R1-tangent
+// (one kernel, conv3x3_kernel) and the weight gradient (wgrad3x3_kernel).
+//
+// Forward = implicit GEMM over an LDS-staged spatial halo tile:
+//   M = output pixels of a TH x TW (x NB images) tile, N = output channels (BN),
+//   K = 9 taps x Cin, walked in chunks of CK input channels.
+// Per chunk the workgroup stages the (TH+2)x(TW+2) NHWC halo (optionally read
+// through a nearest x2 upsample) and the BN x (9*CK) weight slab in LDS, then
+// every wave issues MFMAs whose A fragment is 8 consecutive channels of one halo
+// pixel shifted by the tap and whose B fragment is 8 consecutive (tap,cin) of
+// one output channel: one 16-byte ds_read each.
+//   bf16: v_mfma_f32_16x16x32_bf16 (one per fragment pair)
+//   f32 : v_mfma_f32_16x16x4_f32 x 8 with the k index permuted so lane group g
+//         owns k = 8g..8g+7 (same LDS reads as bf16; exact fp32)
+// Epilogue: accumulators -> LDS tile -> bias / leaky-relu / 2x2 pool / lrelu'
+// mask / accumulate -> coalesced channel-vector stores.
+// Reference: lib/layers.py:58-89 (conv*c incl. bias), lib/blocks.py:113-201.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+namespace {
+
+struct ConvParams {
+  const void* x;
+  const void* w;
+  const float* bias;
+  const void* aux;
+  void* y;
+  void* y2;
+  int B, H, W, Hin, Win;
+  int cin_p, cout, cout_p;
+  int x_cs, y_cs, aux_cs, y2_cs;
+  int flags;
+  float slope, out_scale;
+  int NB, TH, TW, tiles_x, tiles_y;
+  int CK, KS, nchunks;
+  int pixb, wrowb, halo_bytes;
+};
+
+template <typename T>
+struct Frag;
+
+template <>
+struct Frag<bf16_t> {
+  bf16x8_t v;
+  __device__ __forceinline__ void load(const char* p) {
+    v = *reinterpret_cast<const bf16x8_t*>(p);
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4_t& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+  }
+};
+
+template <>
+struct Frag<float> {
+  f32x4_t lo, hi;
+  __device__ __forceinline__ void load(const char* p) {
+    lo = *reinterpret_cast<const f32x4_t*>(p);
+    hi = *reinterpret_cast<const f32x4_t*>(p + 16);
+  }
+  static __device__ __forceinline__ void mma(const Frag& a, const Frag& b, f32x4_t& acc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[i], b.lo[i], acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[i], b.hi[i], acc, 0, 0, 0);
+  }
+};
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
+  constexpr int MT = BM / WM / 16;
+  constexpr int NT = BN / WN / 16;
+  static_assert(WM * WN == 4, "4 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int g = lane >> 4, r = lane & 15;
+
+  int t = blockIdx.x;
+  const int tx0 = (t % p.tiles_x) * p.TW;
+  t /= p.tiles_x;
+  const int ty0 = (t % p.tiles_y) * p.TH;
+  t /= p.tiles_y;
+  const int b0 = t * p.NB;
+  const int n0 = blockIdx.y * BN;
+
+  const int TW2 = p.TW + 2;
+  const int HW2 = (p.TH + 2) * TW2;
+  const int npix_halo = p.NB * HW2;
+  char* halo = smem;
+  char* wl = smem + p.halo_bytes;
+
+  int hoff[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int pm = wm * (BM / WM) + mt * 16 + r;
+    const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+    hoff[mt] = ((nb * (p.TH + 2) + ty) * TW2 + tx) * p.pixb;
+  }
+
+  f32x4_t acc[MT][NT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const bool ups = (p.flags & PG_CONV_UPS_IN) != 0;
+  const int vpp = p.CK * (int)sizeof(T) / 16;  // 16-byte vectors per halo pixel / per tap
+  const int ntap_pad = p.KS * 32 / p.CK;
+
+  for (int ch = 0; ch < p.nchunks; ++ch) {
+    const int c0 = ch * p.CK;
+    __syncthreads();
+    for (int i = tid; i < npix_halo * vpp; i += 256) {
+      const int hp = i / vpp, v = i - hp * vpp;
+      const int nb = hp / HW2, rem = hp - nb * HW2;
+      const int hy = rem / TW2, hx = rem - hy * TW2;
+      const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (b < p.B && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+        const int sy = ups ? (yy >> 1) : yy, sx = ups ? (xx >> 1) : xx;
+        const char* src = (const char*)p.x +
+                          ((((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + c0) * sizeof(T) + v * 16;
+        val = *reinterpret_cast<const u32x4_t*>(src);
+      }
+      *reinterpret_cast<u32x4_t*>(halo + hp * p.pixb + v * 16) = val;
+    }
+    for (int i = tid; i < BN * ntap_pad * vpp; i += 256) {
+      const int row = i / (ntap_pad * vpp), rem = i - row * (ntap_pad * vpp);
+      const int tap = rem / vpp, v = rem - tap * vpp;
+      const int n = n0 + row;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (tap < 9 && n < p.cout_p)
+        val = *reinterpret_cast<const u32x4_t*>(
+            (const char*)p.w + (((size_t)n * 9 + tap) * p.cin_p + c0) * sizeof(T) + v * 16);
+      *reinterpret_cast<u32x4_t*>(wl + row * p.wrowb + tap * p.CK * sizeof(T) + v * 16) = val;
+    }
+    __syncthreads();
+    for (int ks = 0; ks < p.KS; ++ks) {
+      const int k0 = ks * 32 + 8 * g;
+      int tap = k0 / p.CK;
+      const int c = k0 - tap * p.CK;
+      if (tap > 8) tap = 8;  // padded taps: weights are zero, read real data
+      const int toff = ((tap / 3) * TW2 + (tap % 3)) * p.pixb + c * (int)sizeof(T);
+      Frag<T> bfr[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        bfr[nt].load(wl + (wn * (BN / WN) + nt * 16 + r) * p.wrowb + k0 * (int)sizeof(T));
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        Frag<T> afr;
+        afr.load(halo + hoff[mt] + toff);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) Frag<T>::mma(afr, bfr[nt], acc[mt][nt]);
+      }
+    }
+  }
+
+  // ---- epilogue: accumulators -> LDS tile [BM][BN+4] fp32 (bias, lrelu applied)
+  __syncthreads();
+  float* ot = reinterpret_cast<float*>(smem);
+  constexpr int ORS = BN + 4;
+  const bool has_bias = (p.flags & PG_CONV_BIAS) != 0;
+  const bool do_lrelu = (p.flags & PG_CONV_LRELU) != 0;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int nl = wn * (BN / WN) + nt * 16 + r;
+    const int n = n0 + nl;
+    const float bv = (has_bias && n < p.cout) ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pm = wm * (BM / WM) + mt * 16 + 4 * g + j;
+        float v = acc[mt][nt][j] + bv;
+        if (do_lrelu) v = lrelu_f(v, p.slope);
+        ot[pm * ORS + nl] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  constexpr int NV = BN / 4;
+  const bool do_mask = (p.flags & PG_CONV_MASK) != 0;
+  const bool do_acc = (p.flags & PG_CONV_ACCUM) != 0;
+  T* y = reinterpret_cast<T*>(p.y);
+  if (!(p.flags & PG_CONV_POOL)) {
+    for (int i = tid; i < BM * NV; i += 256) {
+      const int pm = i / NV, cv = (i - pm * NV) * 4;
+      const int n = n0 + cv;
+      if (n >= p.cout) continue;
+      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int b = b0 + nb;
+      if (b >= p.B) continue;
+      const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ot[pm * ORS + cv + q] * p.out_scale;
+      if (do_mask) {
+        float a[4];
+        Ty<T>::ld4(reinterpret_cast<const T*>(p.aux) + pix * p.aux_cs + n, a);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] *= lmask_f(a[q], p.slope);
+      }
+      T* dst = y + pix * p.y_cs + n;
+      if (do_acc) {
+        float o[4];
+        Ty<T>::ld4(dst, o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += o[q];
+      }
+      Ty<T>::st4(dst, v);
+    }
+  } else {
+    const int PTW = p.TW >> 1, PTH = p.TH >> 1;
+    const int Ho = p.H >> 1, Wo = p.W >> 1;
+    T* y2 = reinterpret_cast<T*>(p.y2);
+    for (int i = tid; i < (BM / 4) * NV; i += 256) {
+      const int pp = i / NV, cv = (i - pp * NV) * 4;
+      const int n = n0 + cv;
+      if (n >= p.cout) continue;
+      const int ptx = pp % PTW, pty = (pp / PTW) % PTH, nb = pp / (PTW * PTH);
+      const int b = b0 + nb;
+      if (b >= p.B) continue;
+      const int pm00 = (nb * p.TH + 2 * pty) * p.TW + 2 * ptx;
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        v[q] = ot[pm00 * ORS + cv + q] + ot[(pm00 + 1) * ORS + cv + q] +
+               ot[(pm00 + p.TW) * ORS + cv + q] + ot[(pm00 + p.TW + 1) * ORS + cv + q];
+      if (y2) {
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 2; ++dx) {
+            const size_t fpix = ((size_t)b * p.H + ty0 + 2 * pty + dy) * p.W + tx0 + 2 * ptx + dx;
+            float f[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) f[q] = ot[(pm00 + dy * p.TW + dx) * ORS + cv + q];
+            Ty<T>::st4(y2 + fpix * p.y2_cs + n, f);
+          }
+      }
+      const size_t pix = ((size_t)b * Ho + (ty0 >> 1) + pty) * Wo + (tx0 >> 1) + ptx;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= p.out_scale;
+      T* dst = y + pix * p.y_cs + n;
+      if (do_acc) {
+        float o[4];
+        Ty<T>::ld4(dst, o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += o[q];
+      }
+      Ty<T>::st4(dst, v);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// Weight gradient: dW[o][c][tap] += scale * sum_p gz[p][o] * x[p + off(tap)][c]
+// One workgroup = 32 output channels x 32 input channels x 9 taps, walking a
+// contiguous range of spatial pixel tiles (split over blockIdx.z); partial
+// sums are added with fp32 atomics.  MFMA v_mfma_f32_16x16x4_f32 with
+// K = pixels: A[o][p] and B[p][c] are one ds_read_b32 each from the
+// pixel-major LDS tiles (exact fp32; bf16 inputs are widened on staging).
+// --------------------------------------------------------------------------
+struct WgParams {
+  const void* x;
+  const void* gz;
+  float* dw;
+  int B, H, W, Hin, Win;
+  int cin, cout, x_cs, gz_cs;
+  int ups;
+  float scale;
+  int NB, TH, TW, tiles_x, tiles_y, ntiles, tiles_per_split;
+};
+
+constexpr int WG_BO = 32, WG_BC = 32, WG_BP = 128, WG_RS = 33;
+
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* gzl = reinterpret_cast<float*>(smem);  // [WG_BP][WG_RS]
+  float* hal = gzl + WG_BP * WG_RS;               // [NB*(TH+2)*(TW+2)][WG_RS]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int o0 = blockIdx.x * WG_BO, cc0 = blockIdx.y * WG_BC;
+  const int om = (wid >> 1) * 16, cn = (wid & 1) * 16;
+  const int TW2 = p.TW + 2, HW2 = (p.TH + 2) * TW2;
+  const T* x = reinterpret_cast<const T*>(p.x);
+  const T* gz = reinterpret_cast<const T*>(p.gz);
+
+  f32x4_t acc[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int t_begin = blockIdx.z * p.tiles_per_split;
+  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
+  for (int t = t_begin; t < t_end; ++t) {
+    int tt = t;
+    const int tx0 = (tt % p.tiles_x) * p.TW;
+    tt /= p.tiles_x;
+    const int ty0 = (tt % p.tiles_y) * p.TH;
+    tt /= p.tiles_y;
+    const int b0 = tt * p.NB;
+    __syncthreads();
+    // gz tile: WG_BP pixels x 32 output channels
+    for (int i = tid; i < WG_BP * WG_BO; i += 256) {
+      const int pm = i / WG_BO, oc = i - pm * WG_BO;
+      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int b = b0 + nb, o = o0 + oc;
+      float v = 0.f;
+      if (b < p.B && o < p.cout)
+        v = Ty<T>::ld(gz + (((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx) * p.gz_cs + o);
+      gzl[pm * WG_RS + oc] = v;
+    }
+    // x halo: NB*(TH+2)*(TW+2) pixels x 32 input channels
+    for (int i = tid; i < p.NB * HW2 * WG_BC; i += 256) {
+      const int hp = i / WG_BC, ci = i - hp * WG_BC;
+      const int nb = hp / HW2, rem = hp - nb * HW2;
+      const int hy = rem / TW2, hx = rem - hy * TW2;
+      const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1, c = cc0 + ci;
+      float v = 0.f;
+      if (b < p.B && c < p.cin && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+        const int sy = p.ups ? (yy >> 1) : yy, sx = p.ups ? (xx >> 1) : xx;
+        v = Ty<T>::ld(x + (((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + c);
+      }
+      hal[hp * WG_RS + ci] = v;
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < WG_BP; k0 += 4) {
+      const int pm = k0 + g;
+      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int hbase = (nb * (p.TH + 2) + ty) * TW2 + tx;
+      const float a = gzl[pm * WG_RS + om + r];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const float bb = hal[(hbase + (tap / 3) * TW2 + (tap % 3)) * WG_RS + cn + r];
+        acc[tap] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc[tap], 0, 0, 0);
+      }
+    }
+  }
+  // acc[tap][j]: row (o) = om + 4g + j, col (c) = cn + r
+  const int c = cc0 + cn + r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = o0 + om + 4 * g + j;
+    if (o < p.cout && c < p.cin) {
+      float* dst = p.dw + ((size_t)o * p.cin + c) * 9;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) atomicAdd(dst + tap, acc[tap][j] * p.scale);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_kernel(int mode, int cout, int cin, int rows, int kin, const float* w,
+                            float scale, T* out) {
+  // fwd:   out[o][tap][c]  (rows = cout_p, kin = cin_p)
+  // dgrad: out[c][tap][o]  (rows = cin padded to 16, kin = cinp(cout)); W flipped
+  const size_t total = (size_t)rows * 9 * kin;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % kin);
+    const int tap = (int)((i / kin) % 9);
+    const int row = (int)(i / ((size_t)kin * 9));
+    float v = 0.f;
+    if (mode == PG_PACK_FWD) {
+      if (row < cout && k < cin) v = w[((size_t)row * cin + k) * 9 + tap] * scale;
+    } else {
+      if (row < cin && k < cout) v = w[((size_t)k * cin + row) * 9 + (8 - tap)] * scale;
+    }
+    Ty<T>::st(out + i, v);
+  }
+}
+
+template <typename T>
+__global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scale, float* db,
+                                 int pix_per_block) {
+  __shared__ float red[256];
+  const int p0 = blockIdx.x * pix_per_block;
+  const int p1 = min(npix, p0 + pix_per_block);
+  if (C <= 256 && (256 % C) == 0) {
+    const int ppi = 256 / C;  // pixels per iteration
+    const int c = threadIdx.x % C, pi = threadIdx.x / C;
+    float s = 0.f;
+    for (int pp = p0 + pi; pp < p1; pp += ppi) s += Ty<T>::ld(g + (size_t)pp * cs + c);
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float t = 0.f;
+      for (int q = 0; q < ppi; ++q) t += red[q * C + threadIdx.x];
+      atomicAdd(db + threadIdx.x, t * scale);
+    }
+  } else {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float s = 0.f;
+      for (int pp = p0; pp < p1; ++pp) s += Ty<T>::ld(g + (size_t)pp * cs + c);
+      atomicAdd(db + c, s * scale);
+    }
+  }
+}
+
+int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
+
+struct TileCfg {
+  int BM, BN, NB, TH, TW;
+};
+
+TileCfg pick_tile(int H, int W, int BM, int BN) {
+  TileCfg t;
+  t.BM = BM;
+  t.BN = BN;
+  t.TW = W < 16 ? W : 16;
+  t.TH = BM / t.TW;
+  if (t.TH > H) t.TH = H;
+  t.NB = BM / (t.TH * t.TW);
+  return t;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
+                const void* aux, void* y, void* y2, hipStream_t st) {
+  TileCfg tc = pick_tile(d->H, d->W, BM, BN);
+  ConvParams p;
+  p.x = x; p.w = wpk; p.bias = bias; p.aux = aux; p.y = y; p.y2 = y2;
+  p.B = d->B; p.H = d->H; p.W = d->W;
+  const bool ups = (d->flags & PG_CONV_UPS_IN) != 0;
+  p.Hin = ups ? d->H / 2 : d->H;
+  p.Win = ups ? d->W / 2 : d->W;
+  p.cin_p = cinp_of(d->cin);
+  p.cout = d->cout;
+  p.cout_p = (d->cout + 15) & ~15;
+  p.x_cs = d->x_cs; p.y_cs = d->y_cs; p.aux_cs = d->aux_cs; p.y2_cs = d->y2_cs;
+  p.flags = d->flags; p.slope = d->slope; p.out_scale = d->out_scale;
+  p.NB = tc.NB; p.TH = tc.TH; p.TW = tc.TW;
+  p.tiles_x = d->W / tc.TW;
+  p.tiles_y = d->H / tc.TH;
+  p.CK = p.cin_p < 32 ? p.cin_p : 32;
+  p.KS = (9 * p.CK + 31) / 32;
+  p.nchunks = p.cin_p / p.CK;
+  const int pb = p.CK * (int)sizeof(T);
+  p.pixb = pb + (pb >= 64 ? 16 : 0);
+  p.wrowb = p.KS * 32 * (int)sizeof(T) + 16;
+  p.halo_bytes = (tc.NB * (tc.TH + 2) * (tc.TW + 2) * p.pixb + 15) & ~15;
+  const int main_bytes = p.halo_bytes + BN * p.wrowb;
+  const int epi_bytes = BM * (BN + 4) * 4;
+  const int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
+  PG_CHECK_ARG(lds <= 160 * 1024, "conv3x3: LDS %d bytes too large", lds);
+  dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0));
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN>), grid, dim3(256), lds, st, p);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+template <typename T>
+int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
+                  const void* aux, void* y, void* y2, hipStream_t st) {
+  const int cout_p = (d->cout + 15) & ~15;
+  if (cout_p >= 64) return launch_conv<T, 128, 64, 2, 2>(d, x, wpk, bias, aux, y, y2, st);
+  if (cout_p >= 32) return launch_conv<T, 256, 32, 4, 1>(d, x, wpk, bias, aux, y, y2, st);
+  return launch_conv<T, 256, 16, 4, 1>(d, x, wpk, bias, aux, y, y2, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t pg_conv3x3_packed_elems(int mode, int cout, int cin) {
+  if (mode == PG_PACK_FWD) return (size_t)((cout + 15) & ~15) * 9 * cinp_of(cin);
+  return (size_t)((cin + 15) & ~15) * 9 * cinp_of(cout);
+}
+
+int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw, float scale,
+                    void* wpk, void* stream) {
+  PG_CHECK_ARG(w_oihw && wpk && cout > 0 && cin > 0, "conv3x3_pack: bad args");
+  int rows, kin;
+  if (mode == PG_PACK_FWD) {
+    rows = (cout + 15) & ~15;
+    kin = cinp_of(cin);
+  } else {
+    rows = (cin + 15) & ~15;
+    kin = cinp_of(cout);
+  }
+  const size_t total = (size_t)rows * 9 * kin;
+  const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
+                       kin, w_oihw, scale, (float*)wpk);
+  else
+    hipLaunchKernelGGL(pack_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
+                       kin, w_oihw, scale, (bf16_t*)wpk);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                   const float* bias, const void* aux, void* y, void* y2, void* stream) {
+  PG_CHECK_ARG(d && x && wpk && y, "conv3x3_fwd: null pointer");
+  PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4 && (d->H & (d->H - 1)) == 0 &&
+                   (d->W & (d->W - 1)) == 0,
+               "conv3x3_fwd: spatial %dx%d must be powers of two >= 4", d->H, d->W);
+  PG_CHECK_ARG(d->cin > 0 && d->cout > 0 && d->cout % 4 == 0,
+               "conv3x3_fwd: cout %d must be a multiple of 4", d->cout);
+  PG_CHECK_ARG(d->x_cs >= cinp_of(d->cin) && d->x_cs % 8 == 0,
+               "conv3x3_fwd: x channel stride %d < padded cin %d (or not a multiple of 8)", d->x_cs,
+               cinp_of(d->cin));
+  PG_CHECK_ARG(d->y_cs >= d->cout && d->y_cs % 4 == 0, "conv3x3_fwd: bad y channel stride");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_BIAS) || bias, "conv3x3_fwd: BIAS flag without bias");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_MASK) || (aux && d->aux_cs >= d->cout),
+               "conv3x3_fwd: MASK flag without aux");
+  PG_CHECK_ARG(!((d->flags & PG_CONV_MASK) && (d->flags & PG_CONV_POOL)),
+               "conv3x3_fwd: MASK and POOL together are not supported");
+  PG_CHECK_ARG(!y2 || (d->flags & PG_CONV_POOL), "conv3x3_fwd: y2 only with POOL");
+  PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, st);
+  return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, st);
+}
+
+int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
+                     float* dw, void* stream) {
+  PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
+  PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
+  TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
+  WgParams p;
+  p.x = x; p.gz = gz; p.dw = dw;
+  p.B = d->B; p.H = d->H; p.W = d->W;
+  p.ups = (d->flags & PG_CONV_UPS_IN) ? 1 : 0;
+  p.Hin = p.ups ? d->H / 2 : d->H;
+  p.Win = p.ups ? d->W / 2 : d->W;
+  p.cin = d->cin; p.cout = d->cout; p.x_cs = d->x_cs; p.gz_cs = d->y_cs;
+  p.scale = scale;
+  p.NB = tc.NB; p.TH = tc.TH; p.TW = tc.TW;
+  p.tiles_x = d->W / tc.TW;
+  p.tiles_y = d->H / tc.TH;
+  p.ntiles = pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y;
+  const int ot = pg_cdiv(d->cout, WG_BO), ct = pg_cdiv(d->cin, WG_BC);
+  int splits = pg_cdiv(2048, ot * ct);
+  if (splits > p.ntiles) splits = p.ntiles;
+  if (splits < 1) splits = 1;
+  p.tiles_per_split = pg_cdiv(p.ntiles, splits);
+  splits = pg_cdiv(p.ntiles, p.tiles_per_split);
+  const int lds = (WG_BP * WG_RS + tc.NB * (tc.TH + 2) * (tc.TW + 2) * WG_RS) * 4;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(ot, ct, splits);
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(wgrad3x3_kernel<float>, grid, dim3(256), lds, st, p);
+  else
+    hipLaunchKernelGGL(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
+                 void* stream) {
+  PG_CHECK_ARG(g && db && npix > 0 && C > 0 && cs >= C, "bias_grad: bad args");
+  int ppb = 256;
+  int blocks = pg_cdiv(npix, ppb);
+  if (blocks > 2048) {
+    blocks = 2048;
+    ppb = pg_cdiv(npix, blocks);
+    blocks = pg_cdiv(npix, ppb);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(bias_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
+                       (const float*)g, scale, db, ppb);
+  else
+    hipLaunchKernelGGL(bias_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
+                       (const bf16_t*)g, scale, db, ppb);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+}  // extern "C"

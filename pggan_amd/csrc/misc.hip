@@ -1,0 +1,1212 @@
+// Memory-bound kernels of the PGGAN step: PixelNorm, pooling/unpooling with
+// leaky-relu masks, fade-in blends, to/fromRGB 1x1 layers, equalized linears,
+// minibatch-stddev (fwd / bwd / R1 second order), BCE + R1 / WGAN-GP
+// penalties, Adam, latent RNG.  All HBM-bound: NHWC channel vectors of 4,
+// fp32 arithmetic, one pass over each tensor.
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+static thread_local char g_err[512] = "";
+
+void pg_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+namespace {
+
+inline int grid_for(size_t n, int block = 256, int cap = 16384) {
+  size_t g = (n + block - 1) / block;
+  if (g > (size_t)cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+#define GRID_STRIDE(i, n) \
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < (n); i += (size_t)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------- PixelNorm
+// L lanes per pixel (power of two); lane handles channels li*4 + k*4L
+template <typename T>
+__global__ void pixnorm_fwd_kernel(int npix, int C, int cs, int L, const T* x, T* y) {
+  const size_t gt = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t pix = gt / L;
+  const int li = (int)(gt % L);
+  const bool valid = pix < (size_t)npix;
+  float ss = 0.f;
+  if (valid)
+    for (int c = li * 4; c < C; c += 4 * L) {
+      float v[4];
+      Ty<T>::ld4(x + pix * cs + c, v);
+      ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    }
+  for (int o = L >> 1; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (!valid) return;
+  const float r = rsqrtf(ss / (float)C + 1e-8f);
+  for (int c = li * 4; c < C; c += 4 * L) {
+    float v[4];
+    Ty<T>::ld4(x + pix * cs + c, v);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] *= r;
+    Ty<T>::st4(y + pix * cs + c, v);
+  }
+}
+
+template <typename T>
+__global__ void pixnorm_lrelu_bwd_kernel(int npix, int C, int cs, int L, const T* u, const T* gy,
+                                         float slope, int apply_mask, T* gz) {
+  const size_t gt = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t pix = gt / L;
+  const int li = (int)(gt % L);
+  const bool valid = pix < (size_t)npix;
+  float ss = 0.f, sg = 0.f;
+  if (valid)
+    for (int c = li * 4; c < C; c += 4 * L) {
+      float a[4], b[4];
+      Ty<T>::ld4(u + pix * cs + c, a);
+      Ty<T>::ld4(gy + pix * cs + c, b);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ss += a[q] * a[q];
+        sg += a[q] * b[q];
+      }
+    }
+  for (int o = L >> 1; o > 0; o >>= 1) {
+    ss += __shfl_xor(ss, o, 64);
+    sg += __shfl_xor(sg, o, 64);
+  }
+  if (!valid) return;
+  const float r = rsqrtf(ss / (float)C + 1e-8f);
+  const float k = r * r * r * sg / (float)C;
+  for (int c = li * 4; c < C; c += 4 * L) {
+    float a[4], b[4], o[4];
+    Ty<T>::ld4(u + pix * cs + c, a);
+    Ty<T>::ld4(gy + pix * cs + c, b);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[q] = r * b[q] - k * a[q];
+      if (apply_mask) o[q] *= lmask_f(a[q], slope);
+    }
+    Ty<T>::st4(gz + pix * cs + c, o);
+  }
+}
+
+int lanes_for(int C) {
+  int L = C / 4;
+  if (L > 64) L = 64;
+  int p = 1;
+  while (p * 2 <= L) p *= 2;
+  return p;
+}
+
+// ------------------------------------------------------------ elementwise
+template <typename T>
+__global__ void unpool_mask_kernel(int B, int H, int W, int C, int g_cs, const T* g, int y_cs,
+                                   const T* ym, float scale, float slope, int ups, int out_cs,
+                                   T* out) {
+  const int nv = C >> 2;
+  const size_t n = (size_t)B * H * W * nv;
+  GRID_STRIDE(i, n) {
+    const int cv = (int)(i % nv) * 4;
+    const size_t pix = i / nv;
+    const int x = (int)(pix % W);
+    const int yy = (int)((pix / W) % H);
+    const int b = (int)(pix / ((size_t)W * H));
+    size_t gp = pix;
+    if (ups) gp = ((size_t)b * (H >> 1) + (yy >> 1)) * (W >> 1) + (x >> 1);
+    float v[4];
+    Ty<T>::ld4(g + gp * g_cs + cv, v);
+    if (ym) {
+      float m[4];
+      Ty<T>::ld4(ym + pix * y_cs + cv, m);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= lmask_f(m[q], slope);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] *= scale;
+    Ty<T>::st4(out + pix * out_cs + cv, v);
+  }
+}
+
+template <typename T>
+__global__ void avgpool2_kernel(int B, int H, int W, int C, int x_cs, const T* x, int y_cs, T* y) {
+  const int Ho = H >> 1, Wo = W >> 1, nv = C >> 2;
+  const size_t n = (size_t)B * Ho * Wo * nv;
+  GRID_STRIDE(i, n) {
+    const int cv = (int)(i % nv) * 4;
+    const size_t op = i / nv;
+    const int xo = (int)(op % Wo);
+    const int yo = (int)((op / Wo) % Ho);
+    const int b = (int)(op / ((size_t)Wo * Ho));
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float v[4];
+        Ty<T>::ld4(x + (((size_t)b * H + 2 * yo + dy) * W + 2 * xo + dx) * x_cs + cv, v);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] += v[q];
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] *= 0.25f;
+    Ty<T>::st4(y + op * y_cs + cv, s);
+  }
+}
+
+template <typename T>
+__global__ void blend_kernel(size_t n, float a, const T* x, float b, const T* y, T* out) {
+  GRID_STRIDE(i, n) {
+    const float xv = Ty<T>::ld(x + i);
+    const float yv = y ? Ty<T>::ld(y + i) : 0.f;
+    Ty<T>::st(out + i, a * xv + b * yv);
+  }
+}
+
+// ------------------------------------------------------------ RGB layers
+template <typename T>
+__device__ __forceinline__ void dot3(const T* x, int C, const float* w, float o[3]) {
+  o[0] = o[1] = o[2] = 0.f;
+  for (int k = 0; k < C; k += 4) {
+    float v[4];
+    Ty<T>::ld4(x + k, v);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o[0] += v[q] * w[k + q];
+      o[1] += v[q] * w[C + k + q];
+      o[2] += v[q] * w[2 * C + k + q];
+    }
+  }
+}
+
+template <typename T>
+__global__ void rgb_out_kernel(int B, int R, int C, int x_cs, const T* x, const float* w,
+                               const float* b, float c, int Cp, int xp_cs, const T* xp,
+                               const float* wp, const float* bp, float cp, float alpha,
+                               float* img) {
+  const size_t n = (size_t)B * R * R;
+  GRID_STRIDE(i, n) {
+    const int px = (int)(i % R), py = (int)((i / R) % R), bi = (int)(i / ((size_t)R * R));
+    float o[3];
+    dot3(x + i * x_cs, C, w, o);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) o[q] = c * (o[q] + b[q]);
+    if (xp) {
+      const int Rp = R >> 1;
+      const size_t qp = ((size_t)bi * Rp + (py >> 1)) * Rp + (px >> 1);
+      float op[3];
+      dot3(xp + qp * xp_cs, Cp, wp, op);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) o[q] = (1.f - alpha) * (cp * (op[q] + bp[q])) + alpha * o[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) img[(((size_t)bi * 3 + q) * R + py) * R + px] = o[q];
+  }
+}
+
+// gx[pix][k] = f * sum_o g[o][pix(children)] W[o][k]; children = 1 (ups=0) or 4 (ups=1:
+// pix is a half-res pixel, the image is at 2x)
+template <typename T>
+__global__ void rgb_dgrad_kernel(int B, int Rx, int C, int x_cs, const float* w, float f,
+                                 int child, const float* gimg, T* gx) {
+  const int nv = C >> 2;
+  const int Ri = child ? 2 * Rx : Rx;
+  const size_t n = (size_t)B * Rx * Rx * nv;
+  GRID_STRIDE(i, n) {
+    const int kv = (int)(i % nv) * 4;
+    const size_t pix = i / nv;
+    const int px = (int)(pix % Rx), py = (int)((pix / Rx) % Rx), bi = (int)(pix / ((size_t)Rx * Rx));
+    float gs[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const float* gp = gimg + ((size_t)bi * 3 + q) * Ri * Ri;
+      if (child) {
+        const int y0 = 2 * py, x0 = 2 * px;
+        gs[q] = gp[(size_t)y0 * Ri + x0] + gp[(size_t)y0 * Ri + x0 + 1] +
+                gp[(size_t)(y0 + 1) * Ri + x0] + gp[(size_t)(y0 + 1) * Ri + x0 + 1];
+      } else {
+        gs[q] = gp[(size_t)py * Ri + px];
+      }
+    }
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      v[k] = f * (gs[0] * w[kv + k] + gs[1] * w[C + kv + k] + gs[2] * w[2 * C + kv + k]);
+    Ty<T>::st4(gx + pix * x_cs + kv, v);
+  }
+}
+
+// dw[o][k] += f * sum_pix g[o][pix] x[pix][k]; db[o] += f * sum_pix g[o][pix]
+// (x at resolution Rx; child=1: g at 2*Rx summed over 2x2 children)
+template <typename T>
+__global__ void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x, float f, int child,
+                                 const float* gimg, float* dw, float* db, int pix_per_block) {
+  __shared__ float red[256 * 4];
+  const int Ri = child ? 2 * Rx : Rx;
+  const size_t npix = (size_t)B * Rx * Rx;
+  const size_t p0 = (size_t)blockIdx.x * pix_per_block;
+  const size_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
+  auto gval = [&](size_t pix, int q) -> float {
+    const int px = (int)(pix % Rx), py = (int)((pix / Rx) % Rx), bi = (int)(pix / ((size_t)Rx * Rx));
+    const float* gp = gimg + ((size_t)bi * 3 + q) * Ri * Ri;
+    if (!child) return gp[(size_t)py * Ri + px];
+    const int y0 = 2 * py, x0 = 2 * px;
+    return gp[(size_t)y0 * Ri + x0] + gp[(size_t)y0 * Ri + x0 + 1] + gp[(size_t)(y0 + 1) * Ri + x0] +
+           gp[(size_t)(y0 + 1) * Ri + x0 + 1];
+  };
+  if (C <= 256 && 256 % C == 0) {
+    const int ppi = 256 / C, k = threadIdx.x % C, pi = threadIdx.x / C;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (size_t pp = p0 + pi; pp < p1; pp += ppi) {
+      const float xv = Ty<T>::ld(x + pp * x_cs + k);
+      const float g0 = gval(pp, 0), g1 = gval(pp, 1), g2 = gval(pp, 2);
+      a0 += g0 * xv; a1 += g1 * xv; a2 += g2 * xv;
+      if (k == 0) { s0 += g0; s1 += g1; s2 += g2; }
+    }
+    red[threadIdx.x * 4 + 0] = a0; red[threadIdx.x * 4 + 1] = a1; red[threadIdx.x * 4 + 2] = a2;
+    red[threadIdx.x * 4 + 3] = 0.f;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+      for (int q = 0; q < ppi; ++q) {
+        t0 += red[(q * C + threadIdx.x) * 4 + 0];
+        t1 += red[(q * C + threadIdx.x) * 4 + 1];
+        t2 += red[(q * C + threadIdx.x) * 4 + 2];
+      }
+      atomicAdd(dw + threadIdx.x, f * t0);
+      atomicAdd(dw + C + threadIdx.x, f * t1);
+      atomicAdd(dw + 2 * C + threadIdx.x, f * t2);
+    }
+    __syncthreads();
+    red[threadIdx.x * 4 + 0] = s0; red[threadIdx.x * 4 + 1] = s1; red[threadIdx.x * 4 + 2] = s2;
+    __syncthreads();
+    if (threadIdx.x == 0 && db) {
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+      for (int q = 0; q < ppi; ++q) {
+        t0 += red[(q * C) * 4 + 0];
+        t1 += red[(q * C) * 4 + 1];
+        t2 += red[(q * C) * 4 + 2];
+      }
+      atomicAdd(db + 0, f * t0); atomicAdd(db + 1, f * t1); atomicAdd(db + 2, f * t2);
+    }
+  } else {
+    for (int k = threadIdx.x; k < C; k += blockDim.x) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
+      for (size_t pp = p0; pp < p1; ++pp) {
+        const float xv = Ty<T>::ld(x + pp * x_cs + k);
+        const float g0 = gval(pp, 0), g1 = gval(pp, 1), g2 = gval(pp, 2);
+        a0 += g0 * xv; a1 += g1 * xv; a2 += g2 * xv;
+        s0 += g0; s1 += g1; s2 += g2;
+      }
+      atomicAdd(dw + k, f * a0); atomicAdd(dw + C + k, f * a1); atomicAdd(dw + 2 * C + k, f * a2);
+      if (k == 0 && db) { atomicAdd(db + 0, f * s0); atomicAdd(db + 1, f * s1); atomicAdd(db + 2, f * s2); }
+    }
+  }
+}
+
+__device__ __forceinline__ void img_in3(const float* img, int bi, int R, int py, int px, int down,
+                                        float v[3]) {
+  if (!down) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) v[i] = img[(((size_t)bi * 3 + i) * R + py) * R + px];
+  } else {
+    const int Ri = 2 * R;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float* p = img + ((size_t)bi * 3 + i) * Ri * Ri;
+      const size_t a = (size_t)(2 * py) * Ri + 2 * px;
+      v[i] = 0.25f * (p[a] + p[a + 1] + p[a + Ri] + p[a + Ri + 1]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void from_rgb_kernel(int B, int R, int C, const float* img, int down, const float* w,
+                                const float* b, float c, float slope, const T* mask_y, int y_cs,
+                                T* y) {
+  const int nv = C >> 2;
+  const size_t n = (size_t)B * R * R * nv;
+  GRID_STRIDE(i, n) {
+    const int ov = (int)(i % nv) * 4;
+    const size_t pix = i / nv;
+    const int px = (int)(pix % R), py = (int)((pix / R) % R), bi = (int)(pix / ((size_t)R * R));
+    float iv[3];
+    img_in3(img, bi, R, py, px, down, iv);
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = ov + k;
+      float a = iv[0] * w[o * 3] + iv[1] * w[o * 3 + 1] + iv[2] * w[o * 3 + 2];
+      if (b) a += b[o];
+      v[k] = c * a;
+    }
+    if (mask_y) {
+      float m[4];
+      Ty<T>::ld4(mask_y + pix * y_cs + ov, m);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] *= lmask_f(m[k], slope);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = lrelu_f(v[k], slope);
+    }
+    Ty<T>::st4(y + pix * y_cs + ov, v);
+  }
+}
+
+// gimg (at the input resolution) += c * sum_o gz[pix_out][o] W[o][i] (* 0.25 if down)
+template <typename T>
+__global__ void from_rgb_dgrad_kernel(int B, int R, int C, int down, const float* w, float c,
+                                      int gz_cs, const T* gz, float* gimg) {
+  const int Ri = down ? 2 * R : R;
+  const size_t n = (size_t)B * Ri * Ri;
+  const float f = down ? 0.25f * c : c;
+  GRID_STRIDE(i, n) {
+    const int px = (int)(i % Ri), py = (int)((i / Ri) % Ri), bi = (int)(i / ((size_t)Ri * Ri));
+    const int qy = down ? py >> 1 : py, qx = down ? px >> 1 : px;
+    const T* gp = gz + (((size_t)bi * R + qy) * R + qx) * gz_cs;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    for (int o = 0; o < C; o += 4) {
+      float v[4];
+      Ty<T>::ld4(gp + o, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s0 += v[k] * w[(o + k) * 3];
+        s1 += v[k] * w[(o + k) * 3 + 1];
+        s2 += v[k] * w[(o + k) * 3 + 2];
+      }
+    }
+    const size_t plane = (size_t)Ri * Ri;
+    float* dst = gimg + (size_t)bi * 3 * plane + (size_t)py * Ri + px;
+    dst[0] += f * s0;
+    dst[plane] += f * s1;
+    dst[2 * plane] += f * s2;
+  }
+}
+
+// dw[o][i] += c * sum_pix gz[pix][o] img_in[i][pix]; db[o] += c * sum gz[pix][o]
+template <typename T>
+__global__ void from_rgb_wgrad_kernel(int B, int R, int C, const float* img, int down, float c,
+                                      int gz_cs, const T* gz, float* dw, float* db,
+                                      int pix_per_block) {
+  __shared__ float red[256 * 4];
+  const size_t npix = (size_t)B * R * R;
+  const size_t p0 = (size_t)blockIdx.x * pix_per_block;
+  const size_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
+  auto accum = [&](int o, size_t pp0, size_t pp1, size_t step, float a[4]) {
+    for (size_t pp = pp0; pp < pp1; pp += step) {
+      const int px = (int)(pp % R), py = (int)((pp / R) % R), bi = (int)(pp / ((size_t)R * R));
+      float iv[3];
+      img_in3(img, bi, R, py, px, down, iv);
+      const float gv = Ty<T>::ld(gz + pp * gz_cs + o);
+      a[0] += gv * iv[0]; a[1] += gv * iv[1]; a[2] += gv * iv[2]; a[3] += gv;
+    }
+  };
+  if (C <= 256 && 256 % C == 0) {
+    const int ppi = 256 / C, o = threadIdx.x % C, pi = threadIdx.x / C;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    accum(o, p0 + pi, p1, ppi, a);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[threadIdx.x * 4 + q] = a[q];
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < ppi; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] += red[(q * C + threadIdx.x) * 4 + j];
+      if (dw) {
+        atomicAdd(dw + threadIdx.x * 3 + 0, c * t[0]);
+        atomicAdd(dw + threadIdx.x * 3 + 1, c * t[1]);
+        atomicAdd(dw + threadIdx.x * 3 + 2, c * t[2]);
+      }
+      if (db) atomicAdd(db + threadIdx.x, c * t[3]);
+    }
+  } else {
+    for (int o = threadIdx.x; o < C; o += blockDim.x) {
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
+      accum(o, p0, p1, 1, a);
+      if (dw) {
+        atomicAdd(dw + o * 3 + 0, c * a[0]);
+        atomicAdd(dw + o * 3 + 1, c * a[1]);
+        atomicAdd(dw + o * 3 + 2, c * a[2]);
+      }
+      if (db) atomicAdd(db + o, c * a[3]);
+    }
+  }
+}
+
+__global__ void img_fade_kernel(int B, int C, int R, const float* x, float alpha, float* out) {
+  const size_t n = (size_t)B * C * R * R;
+  GRID_STRIDE(i, n) {
+    const int px = (int)(i % R), py = (int)((i / R) % R);
+    const size_t plane = i / ((size_t)R * R);
+    const float* p = x + plane * R * R;
+    const int y0 = py & ~1, x0 = px & ~1;
+    const float lo = 0.25f * (p[(size_t)y0 * R + x0] + p[(size_t)y0 * R + x0 + 1] +
+                              p[(size_t)(y0 + 1) * R + x0] + p[(size_t)(y0 + 1) * R + x0 + 1]);
+    out[i] = (1.f - alpha) * lo + alpha * x[i];
+  }
+}
+
+// ------------------------------------------------------------ linear
+template <typename T>
+struct LinIO {
+  static __device__ __forceinline__ size_t xidx(const pg_linear_desc& d, int b, int k) {
+    if (d.flags & PG_LIN_IN_CHW) {
+      return ((size_t)b * 16 + (k & 15)) * d.in_cs + (k >> 4);
+    }
+    return (size_t)b * d.K + k;
+  }
+  static __device__ __forceinline__ size_t yidx(const pg_linear_desc& d, int b, int n) {
+    if (d.flags & PG_LIN_OUT_CHW) {
+      return ((size_t)b * 16 + (n & 15)) * d.out_cs + (n >> 4);
+    }
+    return (size_t)b * d.N + n;
+  }
+  static __device__ __forceinline__ float ldx(const pg_linear_desc& d, const void* x, size_t i) {
+    return (d.flags & PG_LIN_F32_IN) ? ((const float*)x)[i] : Ty<T>::ld((const T*)x + i);
+  }
+  static __device__ __forceinline__ void stx(const pg_linear_desc& d, void* x, size_t i, float v) {
+    if (d.flags & PG_LIN_F32_IN) ((float*)x)[i] = v;
+    else Ty<T>::st((T*)x + i, v);
+  }
+  static __device__ __forceinline__ float ldy(const pg_linear_desc& d, const void* y, size_t i) {
+    return (d.flags & PG_LIN_F32_OUT) ? ((const float*)y)[i] : Ty<T>::ld((const T*)y + i);
+  }
+  static __device__ __forceinline__ void sty(const pg_linear_desc& d, void* y, size_t i, float v) {
+    if (d.flags & PG_LIN_F32_OUT) ((float*)y)[i] = v;
+    else Ty<T>::st((T*)y + i, v);
+  }
+};
+
+// one wave per output feature n, batch in chunks of 8
+template <typename T>
+__global__ void linear_fwd_kernel(pg_linear_desc d, const void* x, const float* w, const float* b,
+                                  const void* aux, void* y) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (n >= d.N) return;
+  const float* wr = w + (size_t)n * d.K;
+  for (int b0 = 0; b0 < d.B; b0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int k = lane; k < d.K; k += 64) {
+      const float wv = wr[k];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (b0 + q < d.B) acc[q] += wv * LinIO<T>::ldx(d, x, LinIO<T>::xidx(d, b0 + q, k));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = wave_sum(acc[q]);
+    if (lane < 8 && b0 + lane < d.B) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q == lane) v = acc[q];
+      const int bb = b0 + lane;
+      if (d.flags & PG_LIN_BIAS) v += b[n];
+      v *= d.scale;
+      if (d.flags & PG_LIN_LRELU) v = lrelu_f(v, d.slope);
+      const size_t yi = LinIO<T>::yidx(d, bb, n);
+      if (d.flags & PG_LIN_MASK) v *= lmask_f(LinIO<T>::ldy(d, aux, yi), d.slope);
+      LinIO<T>::sty(d, y, yi, v);
+    }
+  }
+}
+
+template <typename T>
+__global__ void linear_dgrad_kernel(pg_linear_desc d, const void* gy, const float* w,
+                                    const void* aux, void* gx) {
+  const size_t n = (size_t)d.B * d.K;
+  GRID_STRIDE(i, n) {
+    const int k = (int)(i % d.K), b = (int)(i / d.K);
+    float s = 0.f;
+    for (int o = 0; o < d.N; ++o)
+      s += LinIO<T>::ldy(d, gy, LinIO<T>::yidx(d, b, o)) * w[(size_t)o * d.K + k];
+    s *= d.scale;
+    const size_t xi = LinIO<T>::xidx(d, b, k);
+    if (d.flags & PG_LIN_MASK) s *= lmask_f(LinIO<T>::ldx(d, aux, xi), d.slope);
+    LinIO<T>::stx(d, gx, xi, s);
+  }
+}
+
+template <typename T>
+__global__ void linear_wgrad_kernel(pg_linear_desc d, const void* x, const void* gy, float* dw,
+                                    float* db) {
+  const size_t n = (size_t)d.N * d.K;
+  GRID_STRIDE(i, n) {
+    const int k = (int)(i % d.K), o = (int)(i / d.K);
+    float s = 0.f, sb = 0.f;
+    for (int b = 0; b < d.B; ++b) {
+      const float gv = LinIO<T>::ldy(d, gy, LinIO<T>::yidx(d, b, o));
+      s += gv * LinIO<T>::ldx(d, x, LinIO<T>::xidx(d, b, k));
+      sb += gv;
+    }
+    dw[i] += d.scale * s;
+    if (k == 0 && db) db[o] += d.scale * sb;
+  }
+}
+
+// ------------------------------------------------------------ minibatch stddev
+__host__ __device__ inline int mbstd_group(int B) {
+  int g = B < 4 ? B : 4;
+  if (B % g != 0) g = B;
+  return g;
+}
+
+template <typename T>
+__global__ void mbstd_fwd_kernel(int B, int HW, int C, int x_cs, const T* x, int y_cs, T* y) {
+  __shared__ float red[16];
+  const int G = mbstd_group(B);
+  const int i0 = blockIdx.x * G;
+  const int E = HW * C;
+  float part = 0.f;
+  if (G > 1) {
+    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+      const int hw = e / C, c = e - hw * C;
+      float mu = 0.f;
+      for (int i = 0; i < G; ++i) mu += Ty<T>::ld(x + ((size_t)(i0 + i) * HW + hw) * x_cs + c);
+      mu /= (float)G;
+      float var = 0.f;
+      for (int i = 0; i < G; ++i) {
+        const float dv = Ty<T>::ld(x + ((size_t)(i0 + i) * HW + hw) * x_cs + c) - mu;
+        var += dv * dv;
+      }
+      var /= (float)(G - 1);
+      part += sqrtf(var + 1e-8f);
+    }
+  }
+  const float s = block_sum(part, red) / (float)E;
+  const size_t n = (size_t)G * HW * y_cs;
+  for (size_t j = threadIdx.x; j < n; j += blockDim.x) {
+    const int c = (int)(j % y_cs);
+    const size_t pix = (size_t)i0 * HW + j / y_cs;
+    float v = 0.f;
+    if (c < C) v = Ty<T>::ld(x + pix * x_cs + c);
+    else if (c == C) v = s;
+    Ty<T>::st(y + pix * y_cs + c, v);
+  }
+}
+
+template <typename T>
+__global__ void mbstd_bwd_kernel(int B, int HW, int C, int x_cs, const T* x, int y_cs,
+                                 const T* gy, T* gx) {
+  __shared__ float red[16];
+  const int G = mbstd_group(B);
+  const int i0 = blockIdx.x * G;
+  const int E = HW * C;
+  float part = 0.f;
+  for (int j = threadIdx.x; j < G * HW; j += blockDim.x)
+    part += Ty<T>::ld(gy + ((size_t)i0 * HW + j) * y_cs + C);
+  const float ds = block_sum(part, red);
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    const int hw = e / C, c = e - hw * C;
+    float mu = 0.f, sig = 1.f;
+    if (G > 1) {
+      for (int i = 0; i < G; ++i) mu += Ty<T>::ld(x + ((size_t)(i0 + i) * HW + hw) * x_cs + c);
+      mu /= (float)G;
+      float var = 0.f;
+      for (int i = 0; i < G; ++i) {
+        const float dv = Ty<T>::ld(x + ((size_t)(i0 + i) * HW + hw) * x_cs + c) - mu;
+        var += dv * dv;
+      }
+      sig = sqrtf(var / (float)(G - 1) + 1e-8f);
+    }
+    const float k = G > 1 ? ds / ((float)E * (float)(G - 1) * sig) : 0.f;
+    for (int i = 0; i < G; ++i) {
+      const size_t pix = (size_t)(i0 + i) * HW + hw;
+      const float xv = Ty<T>::ld(x + pix * x_cs + c);
+      Ty<T>::st(gx + pix * x_cs + c, Ty<T>::ld(gy + pix * y_cs + c) + k * (xv - mu));
+    }
+  }
+}
+
+template <typename T>
+__global__ void mbstd_r1_kernel(int B, int HW, int C, int x_cs, const T* x, const T* a, int y_cs,
+                                const T* gy, T* tout, T* inj) {
+  __shared__ float red[16];
+  const int G = mbstd_group(B);
+  const int i0 = blockIdx.x * G;
+  const int E = HW * C;
+  float part = 0.f;
+  for (int j = threadIdx.x; j < G * HW; j += blockDim.x)
+    part += Ty<T>::ld(gy + ((size_t)i0 * HW + j) * y_cs + C);
+  const float ds = block_sum(part, red);
+  const float K = G > 1 ? ds / ((float)E * (float)(G - 1)) : 0.f;
+  float sp = 0.f;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    const int hw = e / C, c = e - hw * C;
+    if (G == 1) {
+      const size_t pix = (size_t)i0 * HW + hw;
+      Ty<T>::st(inj + pix * x_cs + c, 0.f);
+      continue;
+    }
+    float mu = 0.f, abar = 0.f;
+    for (int i = 0; i < G; ++i) {
+      const size_t pix = (size_t)(i0 + i) * HW + hw;
+      mu += Ty<T>::ld(x + pix * x_cs + c);
+      abar += Ty<T>::ld(a + pix * x_cs + c);
+    }
+    mu /= (float)G;
+    abar /= (float)G;
+    float var = 0.f, A = 0.f;
+    for (int i = 0; i < G; ++i) {
+      const size_t pix = (size_t)(i0 + i) * HW + hw;
+      const float dv = Ty<T>::ld(x + pix * x_cs + c) - mu;
+      var += dv * dv;
+      A += Ty<T>::ld(a + pix * x_cs + c) * dv;
+    }
+    const float sig = sqrtf(var / (float)(G - 1) + 1e-8f);
+    sp += A / sig;
+    const float k3 = A / ((float)(G - 1) * sig * sig * sig);
+    for (int i = 0; i < G; ++i) {
+      const size_t pix = (size_t)(i0 + i) * HW + hw;
+      const float dv = Ty<T>::ld(x + pix * x_cs + c) - mu;
+      const float av = Ty<T>::ld(a + pix * x_cs + c);
+      Ty<T>::st(inj + pix * x_cs + c, K * ((av - abar) / sig - k3 * dv));
+    }
+  }
+  const float sdot = G > 1 ? block_sum(sp, red) / ((float)E * (float)(G - 1)) : 0.f;
+  const size_t n = (size_t)G * HW * y_cs;
+  for (size_t j = threadIdx.x; j < n; j += blockDim.x) {
+    const int c = (int)(j % y_cs);
+    const size_t pix = (size_t)i0 * HW + j / y_cs;
+    float v = 0.f;
+    if (c < C) v = Ty<T>::ld(a + pix * x_cs + c);
+    else if (c == C) v = sdot;
+    Ty<T>::st(tout + pix * y_cs + c, v);
+  }
+}
+
+// ------------------------------------------------------------ losses
+__device__ __forceinline__ float softplus_f(float x) {
+  return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.f / (1.f + expf(-x)); }
+
+__global__ void bce_kernel(int B, const float* l, int target, float w, float* loss, float* u,
+                           float* h) {
+  __shared__ float red[16];
+  float part = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float x = l[b];
+    const float s = sigmoid_f(x);
+    if (target) {
+      part += softplus_f(-x);
+      if (u) u[b] = -w * (1.f - s) / (float)B;
+    } else {
+      part += softplus_f(x);
+      if (u) u[b] = w * s / (float)B;
+    }
+    if (h) h[b] = w * s * (1.f - s) / (float)B;
+  }
+  const float t = block_sum(part, red);
+  if (threadIdx.x == 0 && loss) loss[0] += w * t / (float)B;
+}
+
+__global__ void r1_kernel(int B, size_t n, const float* g, float* r1, float* gbar) {
+  __shared__ float red[16];
+  float part = 0.f;
+  const float inv = 1.f / (float)B;
+  GRID_STRIDE(i, n) {
+    const float v = g[i];
+    part += v * v;
+    if (gbar) gbar[i] = v * inv;
+  }
+  const float t = block_sum(part, red);
+  if (threadIdx.x == 0) atomicAdd(r1, 0.5f * t * inv);
+}
+
+__global__ void gp_interp_kernel(int B, size_t per, const float* xr, const float* xf,
+                                 const float* eps, float* out) {
+  const size_t n = (size_t)B * per;
+  GRID_STRIDE(i, n) {
+    const float e = eps[i / per];
+    out[i] = e * xr[i] + (1.f - e) * xf[i];
+  }
+}
+
+__global__ void sumsq_per_sample_kernel(int B, size_t per, const float* g, float* norms) {
+  __shared__ float red[16];
+  const int b = blockIdx.y;
+  float part = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < per;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const float v = g[(size_t)b * per + i];
+    part += v * v;
+  }
+  const float t = block_sum(part, red);
+  if (threadIdx.x == 0) atomicAdd(norms + b, t);
+}
+
+__global__ void gp_finish_kernel(int B, size_t per, const float* g, float w, const float* sumsq,
+                                 float* gp, float* gbar) {
+  const size_t n = (size_t)B * per;
+  GRID_STRIDE(i, n) {
+    const int b = (int)(i / per);
+    const float nb = sqrtf(sumsq[b]);
+    gbar[i] = nb > 0.f ? w * 2.f * (nb - 1.f) / nb * g[i] : 0.f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float t = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float nb = sqrtf(sumsq[b]);
+      t += (nb - 1.f) * (nb - 1.f);
+    }
+    gp[0] += w * t;
+  }
+}
+
+__global__ void mul_add_kernel(size_t n, const float* x, const float* y, const float* z, float* out) {
+  GRID_STRIDE(i, n) out[i] = x[i] + y[i] * z[i];
+}
+
+// ------------------------------------------------------------ Adam
+__global__ void adam_kernel(size_t n, float* p, const float* g, float* m, float* v, float beta1,
+                            float beta2, float eps, float step_size, float bc2_sqrt) {
+  GRID_STRIDE(i, n) {
+    const float gi = g[i];
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+// ------------------------------------------------------------ RNG / cast
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ void randn_kernel(size_t n, uint64_t seed, uint64_t offset, float* out) {
+  GRID_STRIDE(i, n) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(offset + i));
+    const float u1 = ((float)(uint32_t)(h >> 40) + 0.5f) * (1.f / 16777216.f);
+    const float u2 = ((float)(uint32_t)((h >> 16) & 0xffffffu)) * (1.f / 16777216.f);
+    out[i] = sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
+  }
+}
+
+template <typename A, typename B>
+__global__ void cast_kernel(size_t n, const A* x, B* y) {
+  GRID_STRIDE(i, n) Ty<B>::st(y + i, Ty<A>::ld(x + i));
+}
+
+}  // namespace
+
+#define DT_DISPATCH(dtype, KERNEL, grid, block, shm, st, ...)                                  \
+  do {                                                                                         \
+    if ((dtype) == PG_F32)                                                                     \
+      hipLaunchKernelGGL(KERNEL<float>, grid, block, shm, st, __VA_ARGS__);                    \
+    else if ((dtype) == PG_BF16)                                                               \
+      hipLaunchKernelGGL(KERNEL<bf16_t>, grid, block, shm, st, __VA_ARGS__);                   \
+    else {                                                                                     \
+      pg_set_error("%s: bad dtype %d", __func__, (int)(dtype));                                \
+      return PG_ERR_ARG;                                                                       \
+    }                                                                                          \
+  } while (0)
+
+extern "C" {
+
+const char* pg_last_error(void) { return g_err; }
+int pg_version(void) { return 100; }
+
+int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, void* stream) {
+  PG_CHECK_ARG(x && y && npix > 0 && C % 4 == 0 && cs >= C && cs % 4 == 0, "pixnorm_fwd: bad args");
+  const int L = lanes_for(C);
+  const size_t threads = (size_t)npix * L;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(pixnorm_fwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0, st,
+                       npix, C, cs, L, (const float*)x, (float*)y);
+  else
+    hipLaunchKernelGGL(pixnorm_fwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0, st,
+                       npix, C, cs, L, (const bf16_t*)x, (bf16_t*)y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, const void* gy,
+                         float slope, int apply_mask, void* gz, void* stream) {
+  PG_CHECK_ARG(u && gy && gz && npix > 0 && C % 4 == 0 && cs >= C, "pixnorm_lrelu_bwd: bad args");
+  const int L = lanes_for(C);
+  const size_t threads = (size_t)npix * L;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(pixnorm_lrelu_bwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0,
+                       st, npix, C, cs, L, (const float*)u, (const float*)gy, slope, apply_mask,
+                       (float*)gz);
+  else
+    hipLaunchKernelGGL(pixnorm_lrelu_bwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0,
+                       st, npix, C, cs, L, (const bf16_t*)u, (const bf16_t*)gy, slope, apply_mask,
+                       (bf16_t*)gz);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
+                   const void* y, float scale, float slope, int ups, int out_cs, void* out,
+                   void* stream) {
+  PG_CHECK_ARG(g && out && C % 4 == 0 && (!ups || (H % 2 == 0 && W % 2 == 0)),
+               "unpool_mask: bad args");
+  const size_t n = (size_t)B * H * W * (C / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(unpool_mask_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       g_cs, (const float*)g, y_cs, (const float*)y, scale, slope, ups, out_cs,
+                       (float*)out);
+  else
+    hipLaunchKernelGGL(unpool_mask_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       g_cs, (const bf16_t*)g, y_cs, (const bf16_t*)y, scale, slope, ups, out_cs,
+                       (bf16_t*)out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_avgpool2(int dtype, int B, int H, int W, int C, int x_cs, const void* x, int y_cs, void* y,
+                void* stream) {
+  PG_CHECK_ARG(x && y && C % 4 == 0 && H % 2 == 0 && W % 2 == 0, "avgpool2: bad args");
+  const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(avgpool2_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       x_cs, (const float*)x, y_cs, (float*)y);
+  else
+    hipLaunchKernelGGL(avgpool2_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       x_cs, (const bf16_t*)x, y_cs, (bf16_t*)y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_blend(int dtype, size_t n, float a, const void* x, float b, const void* y, void* out,
+             void* stream) {
+  PG_CHECK_ARG(x && out, "blend: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(blend_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
+                       (const float*)x, b, (const float*)y, (float*)out);
+  else
+    hipLaunchKernelGGL(blend_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
+                       (const bf16_t*)x, b, (const bf16_t*)y, (bf16_t*)out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
+               const float* b, float c, int Cp, int xp_cs, const void* xp, const float* wp,
+               const float* bp, float cp, float alpha, float* img, void* stream) {
+  PG_CHECK_ARG(x && w && b && img && C % 4 == 0 && (!xp || (wp && bp && Cp % 4 == 0 && R % 2 == 0)),
+               "rgb_out: bad args");
+  const size_t n = (size_t)B * R * R;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(rgb_out_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
+                       (const float*)x, w, b, c, Cp, xp_cs, (const float*)xp, wp, bp, cp, alpha, img);
+  else
+    hipLaunchKernelGGL(rgb_out_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
+                       (const bf16_t*)x, w, b, c, Cp, xp_cs, (const bf16_t*)xp, wp, bp, cp, alpha,
+                       img);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+}  // extern "C"
+
+template <typename T>
+static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* w, float c, int Cp,
+                        int xp_cs, const T* xp, const float* wp, float cp, float alpha,
+                        const float* gimg, T* gx, T* gxp, float* dw, float* db, float* dwp,
+                        float* dbp, hipStream_t st) {
+  const float fa = xp ? alpha * c : c;
+  size_t n = (size_t)B * R * R * (C / 4);
+  if (gx)
+    hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs, w,
+                       fa, 0, gimg, gx);
+  {
+    const size_t npix = (size_t)B * R * R;
+    int ppb = 1024;
+    int blocks = (int)((npix + ppb - 1) / ppb);
+    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    if (dw)
+      hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
+                         0, gimg, dw, db, ppb);
+  }
+  if (xp) {
+    const int Rp = R / 2;
+    const float fp = (1.f - alpha) * cp;
+    n = (size_t)B * Rp * Rp * (Cp / 4);
+    if (gxp)
+      hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, Rp, Cp, xp_cs,
+                         wp, fp, 1, gimg, gxp);
+    const size_t npix = (size_t)B * Rp * Rp;
+    int ppb = 1024;
+    int blocks = (int)((npix + ppb - 1) / ppb);
+    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    if (dwp)
+      hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
+                         fp, 1, gimg, dwp, dbp, ppb);
+  }
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+extern "C" {
+
+int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
+                   float c, int Cp, int xp_cs, const void* xp, const float* wp, float cp,
+                   float alpha, const float* gimg, void* gx, void* gxp, float* dw, float* db,
+                   float* dwp, float* dbp, void* stream) {
+  PG_CHECK_ARG(x && w && gimg && C % 4 == 0 && (!xp || (wp && Cp % 4 == 0)), "rgb_out_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    return rgb_bwd_impl<float>(B, R, C, x_cs, (const float*)x, w, c, Cp, xp_cs, (const float*)xp,
+                               wp, cp, alpha, gimg, (float*)gx, (float*)gxp, dw, db, dwp, dbp, st);
+  return rgb_bwd_impl<bf16_t>(B, R, C, x_cs, (const bf16_t*)x, w, c, Cp, xp_cs, (const bf16_t*)xp,
+                              wp, cp, alpha, gimg, (bf16_t*)gx, (bf16_t*)gxp, dw, db, dwp, dbp, st);
+}
+
+int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
+                void* stream) {
+  PG_CHECK_ARG(img && w && y && C % 4 == 0 && y_cs >= C, "from_rgb: bad args");
+  const size_t n = (size_t)B * R * R * (C / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(from_rgb_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
+                       down, w, b, c, slope, (const float*)mask_y, y_cs, (float*)y);
+  else
+    hipLaunchKernelGGL(from_rgb_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
+                       down, w, b, c, slope, (const bf16_t*)mask_y, y_cs, (bf16_t*)y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                    float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
+                    void* stream) {
+  PG_CHECK_ARG(w && gz && C % 4 == 0, "from_rgb_bwd: bad args");
+  PG_CHECK_ARG(!(dw || db) || img, "from_rgb_bwd: wgrad needs img");
+  hipStream_t st = (hipStream_t)stream;
+  if (gimg) {
+    const int Ri = down ? 2 * R : R;
+    const size_t n = (size_t)B * Ri * Ri;
+    if (dtype == PG_F32)
+      hipLaunchKernelGGL(from_rgb_dgrad_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C,
+                         down, w, c, gz_cs, (const float*)gz, gimg);
+    else
+      hipLaunchKernelGGL(from_rgb_dgrad_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R,
+                         C, down, w, c, gz_cs, (const bf16_t*)gz, gimg);
+  }
+  if (dw || db) {
+    const size_t npix = (size_t)B * R * R;
+    int ppb = 1024;
+    int blocks = (int)((npix + ppb - 1) / ppb);
+    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    if (dtype == PG_F32)
+      hipLaunchKernelGGL(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C, img,
+                         down, c, gz_cs, (const float*)gz, dw, db, ppb);
+    else
+      hipLaunchKernelGGL(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
+                         img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
+  }
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_img_fade(int B, int C, int R, const float* x, float alpha, float* out, void* stream) {
+  PG_CHECK_ARG(x && out && R % 2 == 0, "img_fade: bad args");
+  const size_t n = (size_t)B * C * R * R;
+  hipLaunchKernelGGL(img_fade_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, B, C, R,
+                     x, alpha, out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_linear_fwd(int dtype, const pg_linear_desc* d, const void* x, const float* w,
+                  const float* b, const void* aux, void* y, void* stream) {
+  PG_CHECK_ARG(d && x && w && y && d->B > 0 && d->K > 0 && d->N > 0, "linear_fwd: bad args");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_BIAS) || b, "linear_fwd: BIAS without bias");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_fwd: MASK without aux");
+  const int wpb = 4;
+  hipStream_t st = (hipStream_t)stream;
+  DT_DISPATCH(dtype, linear_fwd_kernel, dim3(pg_cdiv(d->N, wpb)), dim3(64 * wpb), 0, st, *d, x, w, b,
+              aux, y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
+                    const void* aux, void* gx, void* stream) {
+  PG_CHECK_ARG(d && gy && w && gx, "linear_dgrad: bad args");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_dgrad: MASK without aux");
+  const size_t n = (size_t)d->B * d->K;
+  hipStream_t st = (hipStream_t)stream;
+  DT_DISPATCH(dtype, linear_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, *d, gy, w, aux, gx);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const void* gy, float* dw,
+                    float* db, void* stream) {
+  PG_CHECK_ARG(d && x && gy && dw, "linear_wgrad: bad args");
+  const size_t n = (size_t)d->N * d->K;
+  hipStream_t st = (hipStream_t)stream;
+  DT_DISPATCH(dtype, linear_wgrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, *d, x, gy, dw, db);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_mbstd_fwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y_cs, void* y,
+                 void* stream) {
+  PG_CHECK_ARG(x && y && B > 0 && y_cs > C && x_cs >= C, "mbstd_fwd: bad args");
+  const int G = mbstd_group(B);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(mbstd_fwd_kernel<float>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+                       (const float*)x, y_cs, (float*)y);
+  else
+    hipLaunchKernelGGL(mbstd_fwd_kernel<bf16_t>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+                       (const bf16_t*)x, y_cs, (bf16_t*)y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+}  // extern "C"
+
+// typed wrappers for the remaining mbstd entry points (DT_DISPATCH needs typed pointers)
+template <typename T>
+static void mbstd_bwd_launch(int B, int HW, int C, int x_cs, const void* x, int y_cs, const void* gy,
+                             void* gx, hipStream_t st) {
+  const int G = mbstd_group(B);
+  hipLaunchKernelGGL(mbstd_bwd_kernel<T>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+                     (const T*)x, y_cs, (const T*)gy, (T*)gx);
+}
+template <typename T>
+static void mbstd_r1_launch(int B, int HW, int C, int x_cs, const void* x, const void* a, int y_cs,
+                            const void* gy, void* tout, void* inj, hipStream_t st) {
+  const int G = mbstd_group(B);
+  hipLaunchKernelGGL(mbstd_r1_kernel<T>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs, (const T*)x,
+                     (const T*)a, y_cs, (const T*)gy, (T*)tout, (T*)inj);
+}
+
+extern "C" {
+
+int pg_mbstd_bwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y_cs,
+                 const void* gy, void* gx, void* stream) {
+  PG_CHECK_ARG(x && gy && gx && B > 0 && y_cs > C, "mbstd_bwd: bad args");
+  if (dtype == PG_F32) mbstd_bwd_launch<float>(B, HW, C, x_cs, x, y_cs, gy, gx, (hipStream_t)stream);
+  else mbstd_bwd_launch<bf16_t>(B, HW, C, x_cs, x, y_cs, gy, gx, (hipStream_t)stream);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_mbstd_r1(int dtype, int B, int HW, int C, int x_cs, const void* x, const void* a, int y_cs,
+                const void* gy, void* tout, void* inj, void* stream) {
+  PG_CHECK_ARG(x && a && gy && tout && inj && B > 0 && y_cs > C, "mbstd_r1: bad args");
+  if (dtype == PG_F32)
+    mbstd_r1_launch<float>(B, HW, C, x_cs, x, a, y_cs, gy, tout, inj, (hipStream_t)stream);
+  else
+    mbstd_r1_launch<bf16_t>(B, HW, C, x_cs, x, a, y_cs, gy, tout, inj, (hipStream_t)stream);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out, float* u,
+                float* h, void* stream) {
+  PG_CHECK_ARG(logits && B > 0, "bce_loss: bad args");
+  hipLaunchKernelGGL(bce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, target, w,
+                     loss_out, u, h);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream) {
+  PG_CHECK_ARG(g && r1_out && B > 0, "r1_penalty: bad args");
+  hipLaunchKernelGGL(r1_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, (hipStream_t)stream, B,
+                     n, g, r1_out, gbar);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_gp_interp(int B, size_t per, const float* xr, const float* xf, const float* eps,
+                 float* out, void* stream) {
+  PG_CHECK_ARG(xr && xf && eps && out, "gp_interp: bad args");
+  hipLaunchKernelGGL(gp_interp_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0,
+                     (hipStream_t)stream, B, per, xr, xf, eps, out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, float* norms,
+                  float* gbar, void* stream) {
+  PG_CHECK_ARG(g && gp_out && norms && gbar, "gp_penalty: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(norms, 0, sizeof(float) * B, st);
+  int gx = grid_for(per, 256, 256);
+  hipLaunchKernelGGL(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms);
+  hipLaunchKernelGGL(gp_finish_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0, st, B, per, g,
+                     w, norms, gp_out, gbar);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_mul_add(size_t n, const float* x, const float* y, const float* z, float* out,
+               void* stream) {
+  PG_CHECK_ARG(x && y && z && out, "mul_add: null pointer");
+  hipLaunchKernelGGL(mul_add_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, y,
+                     z, out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_adam(size_t n, float* p, const float* g, float* m, float* v, float lr, float beta1,
+            float beta2, float eps, int step, void* stream) {
+  PG_CHECK_ARG(p && g && m && v && step >= 1, "adam: bad args");
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
+                     v, beta1, beta2, eps, step_size, bc2_sqrt);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream) {
+  PG_CHECK_ARG(out, "randn: null out");
+  hipLaunchKernelGGL(randn_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, seed,
+                     offset, out);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void* stream) {
+  PG_CHECK_ARG(x && y, "cast: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype_in == PG_F32 && dtype_out == PG_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
+                       (const float*)x, (bf16_t*)y);
+  else if (dtype_in == PG_BF16 && dtype_out == PG_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
+                       (const bf16_t*)x, (float*)y);
+  else if (dtype_in == PG_F32 && dtype_out == PG_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
+                       (const float*)x, (float*)y);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
+                       (const bf16_t*)x, (bf16_t*)y);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+}  // extern "C"

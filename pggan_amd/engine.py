@@ -1,0 +1,624 @@
+"""Hand-scheduled PGGAN training step (G + D + R1) on the HIP kernels.
+
+The reference step (pggan/model.py:206-255) relies on autograd, including a
+double-backward for the R1 penalty (lib/loss.py:125-135).  Here every pass is
+an explicit kernel sequence and the R1 double-backward is derived by hand:
+
+  F   forward of D on the real image, keeping every activation
+  B1  input-gradient pass from u = dL_real/dlogit, keeping the gradient at
+      every pre-activation (gz) and producing g = dL_real/dx
+  R1  r1 = 0.5 mean_b |g_b|^2 ;  gbar = dR1/dg = g / B
+  T   tangent pass: gbar pushed forward through D (the transpose of B1):
+      conv -> *lrelu'(z) -> pool -> blend ...; at every weight layer the R1
+      weight term  dW += c * gz (x) t_in  (the B1 gz paired with the tangent at
+      the layer input) is accumulated.  Two second-order injections appear at
+      the non-piecewise-linear ops: at minibatch-stddev (d/dx <t, J^T gy>) and
+      at the logit (t_out * sigma(l)sigma(-l)/B through the BCE derivative).
+  B2  full backward from u + t_out*h with the mbstd injection added: the weight
+      gradient of L_real plus the indirect part of dR1/dtheta.
+then the fake-image forward/backward (L_fake) and Adam; the G half runs G fwd,
+D fwd, D input-gradient (no D weight gradient: the reference computes and then
+discards it), G backward and Adam.
+
+Activations are NHWC in the engine's storage dtype (fp32 parity mode or bf16),
+images NCHW fp32, parameters/gradients/Adam state fp32 in flat buffers.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+
+SLOPE = 0.2  # blocks hard-code LeakyReLU(0.2) (lib/blocks.py:127,137,185,192,254,283)
+
+
+def cinp(c):
+    """Channel padding the conv kernels expect for their input."""
+    return ((c + 7) // 8) * 8 if c <= 16 else ((c + 31) // 32) * 32
+
+
+def r4(c):
+    return (c + 3) // 4 * 4
+
+
+def he(fan_in):
+    return math.sqrt(2.0 / fan_in)
+
+
+# ---------------------------------------------------------------------------
+# Parameter naming (reference state_dict order, see oracle / SURVEY §8(b))
+# ---------------------------------------------------------------------------
+def g_param_shapes(depths, s, latent_dim=512, out_dim=3):
+    d0 = depths[0]
+    sh = []
+    for i in range(s):
+        p, n = depths[i], depths[i + 1]
+        sh += [(f"blocks.{i}.block.0.module.weight", (n, p, 3, 3)),
+               (f"blocks.{i}.block.0.module.bias", (n,)),
+               (f"blocks.{i}.block.3.module.weight", (n, n, 3, 3)),
+               (f"blocks.{i}.block.3.module.bias", (n,))]
+    for i in range(s + 1):
+        sh += [(f"toRGB_blocks.{i}.toRGB.module.weight", (out_dim, depths[i], 1, 1)),
+               (f"toRGB_blocks.{i}.toRGB.module.bias", (out_dim,))]
+    sh += [("latent_format_layer.module.weight", (16 * d0, latent_dim)),
+           ("latent_format_layer.module.bias", (16 * d0,)),
+           ("first_block.block.0.module.weight", (d0, d0, 3, 3)),
+           ("first_block.block.0.module.bias", (d0,))]
+    return sh
+
+
+def d_param_shapes(depths, s, in_dim=3):
+    d0 = depths[0]
+    sh = []
+    for i in range(s):
+        n, p = depths[i + 1], depths[i]
+        sh += [(f"blocks.{i}.block.0.module.weight", (n, n, 3, 3)),
+               (f"blocks.{i}.block.0.module.bias", (n,)),
+               (f"blocks.{i}.block.2.module.weight", (p, n, 3, 3)),
+               (f"blocks.{i}.block.2.module.bias", (p,))]
+    for i in range(s + 1):
+        sh += [(f"fromRGB_blocks.{i}.fromRGB.module.weight", (depths[i], in_dim, 1, 1)),
+               (f"fromRGB_blocks.{i}.fromRGB.module.bias", (depths[i],))]
+    sh += [("decision_layer.module.weight", (1, d0)),
+           ("decision_layer.module.bias", (1,)),
+           ("minibatch_normalization_block.conv.module.weight", (d0, d0 + 1, 3, 3)),
+           ("minibatch_normalization_block.conv.module.bias", (d0,)),
+           ("minibatch_normalization_block.linear.module.weight", (d0, 16 * d0)),
+           ("minibatch_normalization_block.linear.module.bias", (d0,))]
+    return sh
+
+
+def dead_params(net, s):
+    """Parameters the forward never touches at stage s (their grad stays None in the
+    reference and Adam skips them): toRGB / fromRGB blocks below s-1."""
+    pre = "toRGB_blocks" if net == "G" else "fromRGB_blocks"
+    return {f"{pre}.{j}.{'toRGB' if net == 'G' else 'fromRGB'}.module.{k}"
+            for j in range(max(0, s - 1)) for k in ("weight", "bias")}
+
+
+class FlatParams:
+    """fp32 parameters of one net in one flat buffer (live parameters first) plus
+    flat gradient / Adam-moment buffers; `views[name]` are reference-shaped views."""
+
+    def __init__(self, shapes, dead, device, init=None):
+        order = [n for n, _ in shapes if n not in dead] + [n for n, _ in shapes if n in dead]
+        shp = dict(shapes)
+        self.names = [n for n, _ in shapes]          # reference order
+        self.offsets, off = {}, 0
+        for n in order:
+            self.offsets[n] = off
+            off += int(math.prod(shp[n]))
+        self.numel = off
+        self.n_live = sum(int(math.prod(shp[n])) for n in order if n not in dead)
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.grad = torch.zeros_like(self.flat)
+        self.m = torch.zeros_like(self.flat)
+        self.v = torch.zeros_like(self.flat)
+        self.step = 0
+        self.shapes = shp
+        self.dead = set(dead)
+        self.views = {n: self._view(self.flat, n) for n in self.names}
+        self.gviews = {n: self._view(self.grad, n) for n in self.names}
+        if init is not None:
+            for n in self.names:
+                self.views[n].copy_(init[n])
+
+    def _view(self, buf, n):
+        o = self.offsets[n]
+        return buf[o:o + int(math.prod(self.shapes[n]))].view(self.shapes[n])
+
+    def live_grad(self):
+        return self.grad[:self.n_live]
+
+    def reset_optimizer(self):
+        self.m.zero_()
+        self.v.zero_()
+        self.step = 0
+
+
+# ---------------------------------------------------------------------------
+@dataclass
+class Hyper:
+    lr_G: float = 1e-4
+    lr_D: float = 1e-5
+    beta1: float = 0.0
+    beta2: float = 0.99
+    eps: float = 1e-8
+    W_adv: float = 1.0
+    slope_cfg: float = 0.2      # LReLU_slope (G format layer only, pggan/nets.py:45,129)
+    gp_mode: str = "r1"         # "r1" (live reference path) | "wgan-gp" (optional mode)
+    W_gp: float = 10.0
+
+
+class StepEngine:
+    """All device buffers and kernel schedules for one (stage, batch, dtype)."""
+
+    def __init__(self, ops, depths, s, B, device, latent_dim=512):
+        self.ops, self.depths, self.s, self.B = ops, list(depths), s, B
+        self.dev = device
+        self.dt = ops.tdtype
+        self.latent = latent_dim
+        self.R = 4 * 2 ** s
+        d = self.depths
+        self.d0 = d[0]
+        self.mcs = cinp(d[0] + 1)
+        self.keep_fake_D = False
+        self._alloc()
+
+    # ------------------------------------------------------------------ buffers
+    def _t(self, *shape, f32=False):
+        return torch.zeros(*shape, dtype=torch.float32 if f32 else self.dt, device=self.dev)
+
+    def _alloc(self):
+        B, s, d, R = self.B, self.s, self.depths, self.R
+        t = self._t
+        # ---- G
+        self.g = g = {}
+        g["z"] = t(B, self.latent, f32=True)
+        g["zn"] = t(B, self.latent, f32=True)
+        g["f"] = t(B, 4, 4, d[0])
+        g["h0"] = t(B, 4, 4, d[0])
+        g["u0"] = t(B, 4, 4, d[0])
+        g["y0"] = t(B, 4, 4, d[0])
+        for i in range(s):
+            Ri = 8 * 2 ** i
+            for k in ("ua", "ya", "ub", "yb", "gzb", "gya", "gza"):
+                g[f"{k}{i}"] = t(B, Ri, Ri, d[i + 1])
+        g["img"] = t(B, 3, R, R, f32=True)
+        # gradient wrt level outputs: lvl 0 = y0 (4x4), lvl i+1 = yb_i
+        for j in range(s + 1):
+            Rj = 4 * 2 ** j
+            g[f"gy{j}"] = t(B, Rj, Rj, d[j])
+        g["gz0"] = t(B, 4, 4, d[0])
+        g["gh0"] = t(B, 4, 4, d[0])
+        g["gzf"] = t(B, 4, 4, d[0])
+        # ---- D
+        self.dd = D = {}
+        D["yrgb"] = t(B, R, R, d[s])
+        D["gzrgb"] = t(B, R, R, d[s])
+        D["trgb"] = t(B, R, R, d[s])
+        if s >= 1:
+            D["yd"] = t(B, R // 2, R // 2, d[s - 1])
+            D["gzd"] = t(B, R // 2, R // 2, d[s - 1])
+            D["td"] = t(B, R // 2, R // 2, d[s - 1])
+            D["hblend"] = t(B, R // 2, R // 2, d[s - 1])
+            D["tblend"] = t(B, R // 2, R // 2, d[s - 1])
+        for i in range(s):
+            Ri = 8 * 2 ** i
+            D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
+            D[f"bf{i}"] = t(B, Ri, Ri, d[i])
+            D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
+            D[f"gzb{i}"] = t(B, Ri, Ri, d[i])
+            D[f"gza{i}"] = t(B, Ri, Ri, d[i + 1])
+            D[f"ghin{i}"] = t(B, Ri, Ri, d[i + 1])
+            D[f"ta{i}"] = t(B, Ri, Ri, d[i + 1])
+            D[f"tbf{i}"] = t(B, Ri, Ri, d[i])
+            D[f"tp{i}"] = t(B, Ri // 2, Ri // 2, d[i])
+        D["m"] = t(B, 4, 4, self.mcs)
+        D["c"] = t(B, 4, 4, d[0])
+        D["l1"] = t(B, d[0])
+        D["logit"] = t(B, 1, f32=True)
+        D["gzl1"] = t(B, d[0])
+        D["gzc"] = t(B, 4, 4, d[0])
+        D["gm"] = t(B, 4, 4, self.mcs)
+        D["gh"] = t(B, 4, 4, d[0])
+        D["tm"] = t(B, 4, 4, self.mcs)
+        D["inj"] = t(B, 4, 4, d[0])
+        D["tc"] = t(B, 4, 4, d[0])
+        D["tl1"] = t(B, d[0])
+        D["tout"] = t(B, 1, f32=True)
+        D["u"] = t(B, f32=True)
+        D["u2"] = t(B, f32=True)
+        D["hl"] = t(B, f32=True)
+        D["gimg"] = t(B, 3, R, R, f32=True)
+        D["gbar"] = t(B, 3, R, R, f32=True)
+        D["real"] = t(B, 3, R, R, f32=True)
+        if s >= 1:
+            D["real_in"] = t(B, 3, R, R, f32=True)
+        # WGAN-GP optional mode
+        D["interp"] = t(B, 3, R, R, f32=True)
+        D["gp_eps"] = t(B, 1, f32=True)
+        D["gp_norms"] = t(B, f32=True)
+        D["ones"] = torch.full((B,), 1.0, dtype=torch.float32, device=self.dev)
+        D["zeros"] = torch.zeros((B,), dtype=torch.float32, device=self.dev)
+        # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G
+        self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
+
+    # ------------------------------------------------------------------ weights
+    def _conv_list(self, net):
+        """(key, weight name, cout, cin) of every 3x3 conv of a net at this stage."""
+        d, s = self.depths, self.s
+        out = []
+        if net == "G":
+            out.append(("first", "first_block.block.0.module", d[0], d[0]))
+            for i in range(s):
+                out.append((f"a{i}", f"blocks.{i}.block.0.module", d[i + 1], d[i]))
+                out.append((f"b{i}", f"blocks.{i}.block.3.module", d[i + 1], d[i + 1]))
+        else:
+            out.append(("mb", "minibatch_normalization_block.conv.module", d[0], d[0] + 1))
+            for i in range(s):
+                out.append((f"a{i}", f"blocks.{i}.block.0.module", d[i + 1], d[i + 1]))
+                out.append((f"b{i}", f"blocks.{i}.block.2.module", d[i], d[i + 1]))
+        return out
+
+    def alloc_packs(self):
+        ops = self.ops
+        self.packs = {}
+        for net in ("G", "D"):
+            for key, _, cout, cin in self._conv_list(net):
+                nf = ops.packed_elems(L.PACK_FWD, cout, cin)
+                nd = ops.packed_elems(L.PACK_DGRAD, cout, cin)
+                self.packs[(net, key)] = (
+                    torch.empty(nf, dtype=self.dt, device=self.dev),
+                    torch.empty(nd, dtype=self.dt, device=self.dev),
+                    torch.empty(cout, dtype=torch.float32, device=self.dev),
+                    he(cin * 9))
+
+    def pack(self, net, P):
+        """Fold the He constant into packed fwd/dgrad weights and scaled biases."""
+        if not hasattr(self, "packs"):
+            self.alloc_packs()
+        ops = self.ops
+        for key, wname, cout, cin in self._conv_list(net):
+            pf, pd, bs, c = self.packs[(net, key)]
+            w = P[wname + ".weight"]
+            ops.conv_pack(L.PACK_FWD, w, c, pf)
+            ops.conv_pack(L.PACK_DGRAD, w, c, pd)
+            ops.blend(c, P[wname + ".bias"], 0.0, None, bs)
+
+    # ------------------------------------------------------------------ conv helpers
+    def _conv(self, net, key, x, y, H, cin, cout, flags, aux=None, y2=None, out_scale=1.0,
+              dgrad=False, bias=True):
+        pf, pd, bs, _ = self.packs[(net, key)]
+        if not dgrad and bias:
+            flags |= L.CONV_BIAS
+        self.ops.conv3x3(x, pd if dgrad else pf, y, B=self.B, H=H, W=H, cin=cin, cout=cout,
+                         flags=flags, slope=SLOPE, out_scale=out_scale,
+                         bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2)
+
+    def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False):
+        c = self.packs[(net, key)][3]
+        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c)
+
+    # ================================================================== G
+    def g_forward(self, P, z, alpha):
+        ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
+        if z is not g["z"]:
+            g["z"].copy_(z)
+        ops.pixnorm(g["z"], g["zn"], self.latent)                            # nets.py:124-125
+        Wf = P["latent_format_layer.module.weight"]
+        ops.linear(g["zn"], Wf, P["latent_format_layer.module.bias"], g["f"], B=B,
+                   flags=L.LIN_BIAS | L.LIN_LRELU | L.LIN_OUT_CHW, scale=he(self.latent),
+                   slope=self.hyper.slope_cfg)                                # :129-130
+        ops.pixnorm(g["f"], g["h0"], d[0])                                   # :132-133
+        self._conv("G", "first", g["h0"], g["u0"], 4, d[0], d[0], L.CONV_LRELU)
+        ops.pixnorm(g["u0"], g["y0"], d[0])                                  # blocks.py:131-139
+        prev = g["y0"]
+        for i in range(s):                                                   # nets.py:144-149
+            Ri = 8 * 2 ** i
+            self._conv("G", f"a{i}", prev, g[f"ua{i}"], Ri, d[i], d[i + 1],
+                       L.CONV_UPS_IN | L.CONV_LRELU)
+            ops.pixnorm(g[f"ua{i}"], g[f"ya{i}"], d[i + 1])
+            self._conv("G", f"b{i}", g[f"ya{i}"], g[f"ub{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
+            ops.pixnorm(g[f"ub{i}"], g[f"yb{i}"], d[i + 1])
+            prev = g[f"yb{i}"]
+        self._rgb_out(P, alpha)
+        return g["img"]
+
+    def _ylvl(self, j):
+        return self.g["y0"] if j == 0 else self.g[f"yb{j - 1}"]
+
+    def _rgb_out(self, P, alpha):
+        s, d, g = self.s, self.depths, self.g
+        w = P[f"toRGB_blocks.{s}.toRGB.module.weight"]
+        kw = {}
+        if s >= 1:
+            kw = dict(xp=self._ylvl(s - 1), wp=P[f"toRGB_blocks.{s - 1}.toRGB.module.weight"],
+                      bp=P[f"toRGB_blocks.{s - 1}.toRGB.module.bias"], cp=he(d[s - 1]), Cp=d[s - 1],
+                      alpha=alpha)
+        self.ops.rgb_out(self._ylvl(s), w, P[f"toRGB_blocks.{s}.toRGB.module.bias"], he(d[s]),
+                         g["img"], B=self.B, R=self.R, C=d[s], **kw)   # nets.py:140-156
+
+    def g_backward(self, P, GR, gimg, alpha):
+        ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
+        kw = {}
+        if s >= 1:
+            pre = f"toRGB_blocks.{s - 1}.toRGB.module."
+            kw = dict(xp=self._ylvl(s - 1), wp=P[pre + "weight"], cp=he(d[s - 1]), Cp=d[s - 1],
+                      alpha=alpha, gxp=g[f"gy{s - 1}"], dwp=GR[pre + "weight"],
+                      dbp=GR[pre + "bias"])
+        pre = f"toRGB_blocks.{s}.toRGB.module."
+        ops.rgb_out_bwd(self._ylvl(s), P[pre + "weight"], he(d[s]), gimg, g[f"gy{s}"],
+                        GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s], **kw)
+        for i in reversed(range(s)):
+            Ri = 8 * 2 ** i
+            a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
+            ops.pixnorm_lrelu_bwd(g[f"ub{i}"], g[f"gy{i + 1}"], g[f"gzb{i}"], d[i + 1], SLOPE)
+            self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
+                        d[i + 1])
+            ops.bias_grad(g[f"gzb{i}"], GR[b + "bias"], d[i + 1], self.packs[("G", f"b{i}")][3])
+            self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gya{i}"], Ri, d[i + 1], d[i + 1], 0,
+                       dgrad=True)
+            ops.pixnorm_lrelu_bwd(g[f"ua{i}"], g[f"gya{i}"], g[f"gza{i}"], d[i + 1], SLOPE)
+            self._wgrad("G", f"a{i}", self._ylvl(i), g[f"gza{i}"], GR[a + "weight"], Ri, d[i],
+                        d[i + 1], ups=True)
+            ops.bias_grad(g[f"gza{i}"], GR[a + "bias"], d[i + 1], self.packs[("G", f"a{i}")][3])
+            flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and s >= 1) else 0)
+            self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
+                       dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
+        fb = "first_block.block.0.module."
+        ops.pixnorm_lrelu_bwd(g["u0"], g["gy0"], g["gz0"], d[0], SLOPE)
+        self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0])
+        ops.bias_grad(g["gz0"], GR[fb + "bias"], d[0], self.packs[("G", "first")][3])
+        self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)
+        ops.pixnorm_lrelu_bwd(g["f"], g["gh0"], g["gzf"], d[0], self.hyper.slope_cfg)
+        ops.linear_wgrad(g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
+                         GR["latent_format_layer.module.bias"], B=B, flags=L.LIN_OUT_CHW,
+                         scale=he(self.latent))
+
+    # ================================================================== D
+    def d_forward(self, P, img, alpha):
+        ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        fr = "fromRGB_blocks.{}.fromRGB.module."
+        ops.from_rgb(img, P[fr.format(s) + "weight"], P[fr.format(s) + "bias"], he(3), D["yrgb"],
+                     B=B, R=R, C=d[s], down=False, slope=SLOPE)            # nets.py:255
+        if s >= 1:
+            ops.from_rgb(img, P[fr.format(s - 1) + "weight"], P[fr.format(s - 1) + "bias"], he(3),
+                         D["yd"], B=B, R=R // 2, C=d[s - 1], down=True, slope=SLOPE)  # :251-252
+        h = D["yrgb"]
+        for i in reversed(range(s)):                                           # :260-265
+            Ri = 8 * 2 ** i
+            self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
+            self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
+                       L.CONV_LRELU | L.CONV_POOL, y2=D[f"bf{i}"], out_scale=0.25)
+            if i == s - 1:
+                ops.blend(1.0 - alpha, D["yd"], alpha, D[f"p{i}"], D["hblend"])
+                h = D["hblend"]
+            else:
+                h = D[f"p{i}"]
+        self.h_mb = h
+        ops.mbstd_fwd(h, D["m"], B=B, HW=16, C=d[0])                           # blocks.py:261
+        self._conv("D", "mb", D["m"], D["c"], 4, d[0] + 1, d[0], L.CONV_LRELU)
+        mb = "minibatch_normalization_block.linear.module."
+        ops.linear(D["c"], P[mb + "weight"], P[mb + "bias"], D["l1"], B=B,
+                   flags=L.LIN_BIAS | L.LIN_LRELU | L.LIN_IN_CHW, scale=he(16 * d[0]), slope=SLOPE)
+        ops.linear(D["l1"], P["decision_layer.module.weight"], P["decision_layer.module.bias"],
+                   D["logit"], B=B, flags=L.LIN_BIAS, scale=he(d[0]))          # nets.py:271
+        return D["logit"]
+
+    def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None):
+        """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
+        gimg: accumulate dL/dimg (must be zeroed by the caller); keeps every gz."""
+        ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        dec = "decision_layer.module."
+        lin = "minibatch_normalization_block.linear.module."
+        if GR is not None:
+            ops.linear_wgrad(D["l1"], u, GR[dec + "weight"], GR[dec + "bias"], B=B, flags=0,
+                             scale=he(d[0]))
+        ops.linear_dgrad(u, P[dec + "weight"], D["gzl1"], B=B, flags=L.LIN_MASK, scale=he(d[0]),
+                         slope=SLOPE, aux=D["l1"])
+        if GR is not None:
+            ops.linear_wgrad(D["c"], D["gzl1"], GR[lin + "weight"], GR[lin + "bias"], B=B,
+                             flags=L.LIN_IN_CHW, scale=he(16 * d[0]))
+        ops.linear_dgrad(D["gzl1"], P[lin + "weight"], D["gzc"], B=B,
+                         flags=L.LIN_IN_CHW | L.LIN_MASK, scale=he(16 * d[0]), slope=SLOPE,
+                         aux=D["c"])
+        if GR is not None:
+            cv = "minibatch_normalization_block.conv.module."
+            self._wgrad("D", "mb", D["m"], D["gzc"], GR[cv + "weight"], 4, d[0] + 1, d[0])
+            ops.bias_grad(D["gzc"], GR[cv + "bias"], d[0], self.packs[("D", "mb")][3])
+        self._conv("D", "mb", D["gzc"], D["gm"], 4, d[0], r4(d[0] + 1), 0, dgrad=True)
+        ops.mbstd_bwd(self.h_mb, D["gm"], D["gh"], B=B, HW=16, C=d[0])
+        if inj_mbstd is not None:
+            ops.blend(1.0, D["gh"], 1.0, inj_mbstd, D["gh"])
+        g = D["gh"]
+        for i in range(s):
+            Ri = 8 * 2 ** i
+            a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
+            if i == s - 1:
+                # blend backward: the low-res branch gets (1-alpha) g (nets.py:263-265)
+                ops.unpool_mask(g, D["yd"], D["gzd"], B=B, H=Ri // 2, W=Ri // 2, C=d[i],
+                                scale=1.0 - alpha, slope=SLOPE, ups=False)
+            sc = 0.25 * (alpha if i == s - 1 else 1.0)
+            ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
+                            slope=SLOPE, ups=True)
+            if GR is not None:
+                self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
+                            d[i])
+                ops.bias_grad(D[f"gzb{i}"], GR[b + "bias"], d[i], self.packs[("D", f"b{i}")][3])
+            self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_MASK,
+                       aux=D[f"a{i}"], dgrad=True)
+            hin = D["yrgb"] if i == s - 1 else (D["hblend"] if i == s - 2 else D[f"p{i + 1}"])
+            if GR is not None:
+                self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
+                            d[i + 1])
+                ops.bias_grad(D[f"gza{i}"], GR[a + "bias"], d[i + 1], self.packs[("D", f"a{i}")][3])
+            if i == s - 1:
+                self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
+                           L.CONV_MASK, aux=D["yrgb"], dgrad=True)
+            else:
+                self._conv("D", f"a{i}", D[f"gza{i}"], D[f"ghin{i}"], Ri, d[i + 1], d[i + 1], 0,
+                           dgrad=True)
+                g = D[f"ghin{i}"]
+        if s == 0:
+            ops.unpool_mask(D["gh"], D["yrgb"], D["gzrgb"], B=B, H=4, W=4, C=d[0], scale=1.0,
+                            slope=SLOPE, ups=False)
+        fr = "fromRGB_blocks.{}.fromRGB.module."
+        w = P[fr.format(s) + "weight"]
+        if GR is not None:
+            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
+                             dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
+        if gimg is not None:
+            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg)
+        if s >= 1:
+            w1 = P[fr.format(s - 1) + "weight"]
+            if GR is not None:
+                ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True, img=img,
+                                 dw=GR[fr.format(s - 1) + "weight"],
+                                 db=GR[fr.format(s - 1) + "bias"])
+            if gimg is not None:
+                ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True,
+                                 gimg=gimg)
+
+    def d_tangent(self, P, GR, gbar, u, alpha):
+        """Push gbar (= dR1/dx-gradient) forward through D with the B1 masks, adding the R1
+        weight terms; returns (tangent logit, mbstd injection) for the B2 pass."""
+        ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        fr = "fromRGB_blocks.{}.fromRGB.module."
+        ops.from_rgb(gbar, P[fr.format(s) + "weight"], None, he(3), D["trgb"], B=B, R=R, C=d[s],
+                     down=False, slope=SLOPE, mask_y=D["yrgb"])
+        ops.from_rgb_bwd(D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
+                         down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
+        if s >= 1:
+            ops.from_rgb(gbar, P[fr.format(s - 1) + "weight"], None, he(3), D["td"], B=B, R=R // 2,
+                         C=d[s - 1], down=True, slope=SLOPE, mask_y=D["yd"])
+            ops.from_rgb_bwd(D["gzd"], P[fr.format(s - 1) + "weight"], he(3), B=B, R=R // 2,
+                             C=d[s - 1], down=True, img=gbar, dw=GR[fr.format(s - 1) + "weight"])
+        t = D["trgb"]
+        for i in reversed(range(s)):
+            Ri = 8 * 2 ** i
+            a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
+            self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
+                       aux=D[f"a{i}"], bias=False)
+            self._wgrad("D", f"a{i}", t, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1], d[i + 1])
+            self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tbf{i}"], Ri, d[i + 1], d[i], L.CONV_MASK,
+                       aux=D[f"bf{i}"], bias=False)
+            self._wgrad("D", f"b{i}", D[f"ta{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
+                        d[i])
+            ops.avgpool2(D[f"tbf{i}"], D[f"tp{i}"], B=B, H=Ri, W=Ri, C=d[i])
+            if i == s - 1:
+                ops.blend(1.0 - alpha, D["td"], alpha, D[f"tp{i}"], D["tblend"])
+                t = D["tblend"]
+            else:
+                t = D[f"tp{i}"]
+        ops.mbstd_r1(self.h_mb, t, D["gm"], D["tm"], D["inj"], B=B, HW=16, C=d[0])
+        cv = "minibatch_normalization_block.conv.module."
+        self._conv("D", "mb", D["tm"], D["tc"], 4, d[0] + 1, d[0], L.CONV_MASK, aux=D["c"],
+                   bias=False)
+        self._wgrad("D", "mb", D["tm"], D["gzc"], GR[cv + "weight"], 4, d[0] + 1, d[0])
+        lin = "minibatch_normalization_block.linear.module."
+        ops.linear(D["tc"], P[lin + "weight"], None, D["tl1"], B=B,
+                   flags=L.LIN_IN_CHW | L.LIN_MASK, scale=he(16 * d[0]), slope=SLOPE, aux=D["l1"])
+        ops.linear_wgrad(D["tc"], D["gzl1"], GR[lin + "weight"], None, B=B, flags=L.LIN_IN_CHW,
+                         scale=he(16 * d[0]))
+        dec = "decision_layer.module."
+        ops.linear(D["tl1"], P[dec + "weight"], None, D["tout"], B=B, flags=0, scale=he(d[0]))
+        ops.linear_wgrad(D["tl1"], u, GR[dec + "weight"], None, B=B, flags=0, scale=he(d[0]))
+        return D["tout"], D["inj"]
+
+    # ================================================================== step
+    def d_step(self, PG, PD, GD, real, z, alpha_G, alpha_D, gp_eps=None):
+        """D half of train_step (pggan/model.py:211-238).  Returns the faded real image and
+        the fake image.  Gradients are written to GD (zeroed here)."""
+        ops, D, B, hp = self.ops, self.dd, self.B, self.hyper
+        GD_flat = self._GD_flat
+        GD_flat.zero_()
+        self.loss[:3].zero_()
+        if self.s:
+            ops.img_fade(real, alpha_D, D["real_in"])                       # :217-221
+            xr = D["real_in"]
+        else:
+            xr = real
+        if hp.gp_mode == "r1":
+            # ---- real: F, B1, R1, T, B2
+            self.d_forward(PD, xr, alpha_D)
+            ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], D["hl"])   # lib/loss.py:119-123
+            D["gimg"].zero_()
+            self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
+            ops.r1_penalty(D["gimg"], B, self.loss[2:3], D["gbar"])          # lib/loss.py:125-135
+            tout, inj = self.d_tangent(PD, GD, D["gbar"], D["u"], alpha_D)
+            ops.mul_add(D["u"], tout.view(-1), D["hl"], D["u2"])
+            self.d_backward(PD, GD, D["u2"], alpha_D, img=xr, inj_mbstd=inj)
+        else:
+            self.d_forward(PD, xr, alpha_D)
+            ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
+            self.d_backward(PD, GD, D["u"], alpha_D, img=xr)
+        # ---- fake
+        img_fake = self.g_forward(PG, z, alpha_G)                               # :226-227
+        if self.keep_fake_D:
+            img_fake = img_fake.clone()
+        self.d_forward(PD, img_fake, alpha_D)                                   # :228
+        ops.bce(D["logit"], False, 1.0, self.loss[1:2], D["u"], None)
+        self.d_backward(PD, GD, D["u"], alpha_D, img=img_fake)
+        if hp.gp_mode != "r1":
+            self._wgan_gp(PD, GD, xr, img_fake, gp_eps, alpha_D)
+        return xr, img_fake
+
+    def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
+        """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm."""
+        ops, D, B = self.ops, self.dd, self.B
+        D["gp_eps"].copy_(eps)
+        ops.gp_interp(xr, xf, D["gp_eps"], D["interp"])
+        self.d_forward(PD, D["interp"], alpha)
+        D["gimg"].zero_()
+        self.d_backward(PD, None, D["ones"], alpha, gimg=D["gimg"])     # d(sum D)/dx
+        ops.gp_penalty(D["gimg"], self.hyper.W_gp, self.loss[2:3], D["gp_norms"], D["gbar"])
+        tout, inj = self.d_tangent(PD, GD, D["gbar"], D["ones"], alpha)
+        # upstream of the second backward: no BCE here, so no logit injection
+        self.d_backward(PD, GD, D["zeros"], alpha, img=D["interp"], inj_mbstd=inj)
+
+    def g_step(self, PG, PD, GG, z, alpha_G, alpha_D):
+        """G half of train_step (pggan/model.py:244-253)."""
+        ops, D, hp = self.ops, self.dd, self.hyper
+        self._GG_flat.zero_()
+        self.loss[3:4].zero_()
+        img = self.g_forward(PG, z, alpha_G)
+        self.d_forward(PD, img, alpha_D)
+        ops.bce(D["logit"], True, hp.W_adv, self.loss[3:4], D["u"], None)   # pggan/loss.py:5-14
+        D["gimg"].zero_()
+        self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
+        self.g_backward(PG, GG, D["gimg"], alpha_G)
+        return img
+
+    def bind(self, fpG: FlatParams, fpD: FlatParams, hyper: Hyper):
+        self.fpG, self.fpD, self.hyper = fpG, fpD, hyper
+        self._GD_flat, self._GG_flat = fpD.grad, fpG.grad
+
+    def adam(self, fp: FlatParams, lr):
+        hp = self.hyper
+        fp.step += 1
+        n = fp.n_live
+        self.ops.adam(fp.flat[:n], fp.grad[:n], fp.m[:n], fp.v[:n], lr=lr, beta1=hp.beta1,
+                      beta2=hp.beta2, eps=hp.eps, step=fp.step)
+
+    def train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
+        """One full step: D half (R1) + Adam_D, G half + Adam_G (pggan/model.py:206-255).
+        grad_hook(net, flat_live_grad) runs before each Adam (DP all-reduce)."""
+        fpG, fpD, hp = self.fpG, self.fpD, self.hyper
+        PG, PD = fpG.views, fpD.views
+        self.pack("G", PG)
+        self.pack("D", PD)
+        img_real, img_fake_D = self.d_step(PG, PD, fpD.gviews, real, z1, alpha_G, alpha_D,
+                                           gp_eps=gp_eps)
+        if grad_hook is not None:
+            grad_hook("D", fpD.live_grad())
+        self.adam(fpD, hp.lr_D)
+        self.pack("D", PD)
+        img_fake = self.g_step(PG, PD, fpG.gviews, z2, alpha_G, alpha_D)
+        if grad_hook is not None:
+            grad_hook("G", fpG.live_grad())
+        self.adam(fpG, hp.lr_G)
+        return img_real, img_fake_D, img_fake

@@ -1,0 +1,321 @@
+"""CPU test double of pggan_amd._lib.HipOps — TEST INFRASTRUCTURE ONLY.
+
+Implements every tensor-level op of the HIP C ABI (same argument meaning, same
+packed-weight layouts, NHWC activations with channel strides) with plain
+PyTorch on the CPU.  It exists so that `-m "not gpu"` tests can check the host
+logic of pggan_amd (the hand-scheduled R1 double-backward in engine.py, the
+flat-parameter bookkeeping, the DP contract) against the oracle without a GPU.
+The product never imports this module; on a GPU the engine runs HipOps only.
+The mbstd second-order pieces are computed here with autograd, an independent
+derivation of the closed-form kernel in misc.hip.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
+LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW = 1, 2, 4, 8, 16
+
+
+def cinp(c):
+    return ((c + 7) // 8) * 8 if c <= 16 else ((c + 31) // 32) * 32
+
+
+def r16(c):
+    return (c + 15) // 16 * 16
+
+
+def lmask(y, slope):
+    return torch.where(y > 0, torch.ones_like(y), torch.full_like(y, slope))
+
+
+def nchw(x, C):
+    return x[..., :C].permute(0, 3, 1, 2)
+
+
+def up2(x):  # NCHW nearest x2
+    return x.repeat_interleave(2, 2).repeat_interleave(2, 3)
+
+
+def mbstd_ref(x):
+    """x: [B,HW,C] -> [B,HW,C+1] (lib/blocks.py:204-233 on the NHWC view)."""
+    B = x.shape[0]
+    g = min(B, 4)
+    if B % g:
+        g = B
+    if g == 1:
+        return torch.cat([x, torch.zeros_like(x[..., :1])], -1)
+    y = x.reshape(B // g, g, -1)
+    s = torch.sqrt(y.var(1) + 1e-8).mean(1)                # [groups]
+    ch = s.repeat_interleave(g).view(B, 1, 1).expand(B, x.shape[1], 1)
+    return torch.cat([x, ch], -1)
+
+
+class CpuOps:
+    def __init__(self, dtype=torch.float32):
+        assert dtype == torch.float32
+        self.tdtype = dtype
+
+    # -- conv ------------------------------------------------------------
+    def packed_elems(self, mode, cout, cin):
+        if mode == 0:
+            return r16(cout) * 9 * cinp(cin)
+        return r16(cin) * 9 * cinp(cout)
+
+    def conv_pack(self, mode, w, scale, out):
+        cout, cin = w.shape[:2]
+        w9 = w.reshape(cout, cin, 9)
+        if mode == 0:
+            P = torch.zeros(r16(cout), 9, cinp(cin))
+            P[:cout, :, :cin] = scale * w9.permute(0, 2, 1)
+        else:
+            P = torch.zeros(r16(cin), 9, cinp(cout))
+            P[:cin, :, :cout] = scale * w9.flip(2).permute(1, 2, 0)
+        out.copy_(P.reshape(-1))
+
+    def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
+                bias=None, aux=None, y2=None):
+        ci, co = cinp(cin), r16(cout)
+        Wt = wpk.view(co, 9, ci).permute(0, 2, 1).reshape(co, ci, 3, 3)[:cout]
+        xin = nchw(x, ci)
+        if flags & CONV_UPS_IN:
+            xin = up2(xin)
+        z = F.conv2d(xin, Wt, padding=1)
+        if flags & CONV_BIAS:
+            z = z + bias.view(1, -1, 1, 1)
+        if flags & CONV_LRELU:
+            z = F.leaky_relu(z, slope)
+        z = z.permute(0, 2, 3, 1)                       # NHWC [B,H,W,cout]
+        if flags & CONV_POOL:
+            if y2 is not None:
+                y2[..., :cout] = z
+            z = F.avg_pool2d(z.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4.0
+        z = z * out_scale
+        if flags & CONV_MASK:
+            z = z * lmask(aux[..., :cout], slope)
+        if flags & CONV_ACCUM:
+            y[..., :cout] += z
+        else:
+            y[..., :cout] = z
+
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale):
+        xin = nchw(x, cin)
+        if ups:
+            xin = up2(xin)
+        g = nchw(gz, cout)
+        dw += scale * torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), g, padding=1)
+
+    def bias_grad(self, g, db, C, scale):
+        db += scale * g[..., :C].reshape(-1, C).sum(0)
+
+    # -- pixel norm --------------------------------------------------------
+    def pixnorm(self, x, y, C):
+        v = x[..., :C]
+        y[..., :C] = v * ((v * v).mean(-1, keepdim=True) + 1e-8).rsqrt()
+
+    def pixnorm_lrelu_bwd(self, u, gy, gz, C, slope, mask=True):
+        a, b = u[..., :C], gy[..., :C]
+        r = ((a * a).mean(-1, keepdim=True) + 1e-8).rsqrt()
+        o = r * b - (r ** 3 / C) * a * (a * b).sum(-1, keepdim=True)
+        if mask:
+            o = o * lmask(a, slope)
+        gz[..., :C] = o
+
+    # -- elementwise -------------------------------------------------------
+    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):
+        v = g[..., :C]
+        if ups:
+            v = v.repeat_interleave(2, 1).repeat_interleave(2, 2)
+        v = v * scale
+        if y is not None:
+            v = v * lmask(y[..., :C], slope)
+        out[..., :C] = v
+
+    def avgpool2(self, x, y, *, B, H, W, C):
+        y[..., :C] = F.avg_pool2d(nchw(x, C), 2).permute(0, 2, 3, 1)
+
+    def blend(self, a, x, b, y, out):
+        out.copy_(a * x + (b * y if y is not None else 0.0))
+
+    # -- RGB ---------------------------------------------------------------
+    def rgb_out(self, x, w, b, c, img, *, B, R, C, xp=None, wp=None, bp=None, cp=0.0, Cp=0,
+                alpha=1.0):
+        o = c * (x[..., :C] @ w.view(3, C).t() + b)
+        o = o.permute(0, 3, 1, 2)
+        if xp is not None:
+            op = cp * (xp[..., :Cp] @ wp.view(3, Cp).t() + bp)
+            o = (1 - alpha) * up2(op.permute(0, 3, 1, 2)) + alpha * o
+        img.copy_(o)
+
+    def rgb_out_bwd(self, x, w, c, gimg, gx, dw, db, *, B, R, C, xp=None, wp=None, cp=0.0, Cp=0,
+                    alpha=1.0, gxp=None, dwp=None, dbp=None):
+        fa = alpha * c if xp is not None else c
+        g = gimg.permute(0, 2, 3, 1)
+        gx[..., :C] = fa * g @ w.view(3, C)
+        dw.view(3, C).add_(fa * torch.einsum("bhwo,bhwk->ok", g, x[..., :C]))
+        db.add_(fa * g.reshape(-1, 3).sum(0))
+        if xp is not None:
+            fp = (1 - alpha) * cp
+            gs = F.avg_pool2d(gimg, 2).permute(0, 2, 3, 1) * 4.0
+            if gxp is not None:
+                gxp[..., :Cp] = fp * gs @ wp.view(3, Cp)
+            dwp.view(3, Cp).add_(fp * torch.einsum("bhwo,bhwk->ok", gs, xp[..., :Cp]))
+            dbp.add_(fp * gs.reshape(-1, 3).sum(0))
+
+    def _img_in(self, img, down):
+        iv = F.avg_pool2d(img, 2) if down else img
+        return iv.permute(0, 2, 3, 1)
+
+    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
+        a = self._img_in(img, down) @ w.view(C, 3).t()
+        if b is not None:
+            a = a + b
+        a = c * a
+        if mask_y is not None:
+            a = a * lmask(mask_y[..., :C], slope)
+        else:
+            a = F.leaky_relu(a, slope)
+        y[..., :C] = a
+
+    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None):
+        g = gz[..., :C]
+        if gimg is not None:
+            gi = (c * g @ w.view(C, 3)).permute(0, 3, 1, 2)
+            if down:
+                gi = up2(gi) * 0.25
+            gimg += gi
+        if dw is not None or db is not None:
+            iv = self._img_in(img, down)
+            if dw is not None:
+                dw.view(C, 3).add_(c * torch.einsum("bhwo,bhwi->oi", g, iv))
+            if db is not None:
+                db.add_(c * g.reshape(-1, C).sum(0))
+
+    def img_fade(self, x, alpha, out):
+        out.copy_((1 - alpha) * up2(F.avg_pool2d(x, 2)) + alpha * x)
+
+    # -- linear ------------------------------------------------------------
+    def _X(self, t, flags, K, B):
+        if flags & LIN_IN_CHW:
+            C = K // 16
+            return t.reshape(B, 16, -1)[..., :C].permute(0, 2, 1).reshape(B, K)
+        return t.reshape(B, K)
+
+    def _Y(self, t, flags, N, B):
+        if flags & LIN_OUT_CHW:
+            C = N // 16
+            return t.reshape(B, 16, -1)[..., :C].permute(0, 2, 1).reshape(B, N)
+        return t.reshape(B, N)
+
+    def _setX(self, t, flags, K, B, v):
+        if flags & LIN_IN_CHW:
+            C = K // 16
+            t.view(B, 16, -1)[..., :C] = v.view(B, C, 16).permute(0, 2, 1)
+        else:
+            t.view(B, K).copy_(v)
+
+    def _setY(self, t, flags, N, B, v):
+        if flags & LIN_OUT_CHW:
+            C = N // 16
+            t.view(B, 16, -1)[..., :C] = v.view(B, C, 16).permute(0, 2, 1)
+        else:
+            t.view(B, N).copy_(v)
+
+    def linear(self, x, w, b, y, *, B, flags, scale, slope=0.2, aux=None):
+        N, K = w.shape
+        o = self._X(x, flags, K, B) @ w.t()
+        if flags & LIN_BIAS:
+            o = o + b
+        o = o * scale
+        if flags & LIN_LRELU:
+            o = F.leaky_relu(o, slope)
+        if flags & LIN_MASK:
+            o = o * lmask(self._Y(aux, flags, N, B), slope)
+        self._setY(y, flags, N, B, o)
+
+    def linear_dgrad(self, gy, w, gx, *, B, flags, scale, slope=0.2, aux=None):
+        N, K = w.shape
+        o = scale * self._Y(gy, flags, N, B) @ w
+        if flags & LIN_MASK:
+            o = o * lmask(self._X(aux, flags, K, B), slope)
+        self._setX(gx, flags, K, B, o)
+
+    def linear_wgrad(self, x, gy, dw, db, *, B, flags, scale):
+        N, K = dw.shape
+        GY = self._Y(gy, flags, N, B)
+        dw += scale * GY.t() @ self._X(x, flags, K, B)
+        if db is not None:
+            db += scale * GY.sum(0)
+
+    # -- minibatch stddev -----------------------------------------------------
+    def mbstd_fwd(self, x, y, *, B, HW, C):
+        y.zero_()
+        y.view(B, HW, -1)[..., :C + 1] = mbstd_ref(x.reshape(B, HW, -1)[..., :C])
+
+    def mbstd_bwd(self, x, gy, gx, *, B, HW, C):
+        xr = x.reshape(B, HW, -1)[..., :C].detach().clone().requires_grad_()
+        out = mbstd_ref(xr)
+        g, = torch.autograd.grad(out, xr, gy.reshape(B, HW, -1)[..., :C + 1])
+        gx.view(B, HW, -1)[..., :C] = g
+
+    def mbstd_r1(self, x, a, gy, tout, inj, *, B, HW, C):
+        xr = x.reshape(B, HW, -1)[..., :C].detach().clone().requires_grad_()
+        av = a.reshape(B, HW, -1)[..., :C]
+        gyv = gy.reshape(B, HW, -1)[..., :C + 1].detach().clone().requires_grad_()
+        out = mbstd_ref(xr)
+        gx, = torch.autograd.grad(out, xr, gyv, create_graph=True)
+        Fv = (gx * av).sum()
+        ix, igy = torch.autograd.grad(Fv, [xr, gyv], allow_unused=True)
+        inj.view(B, HW, -1)[..., :C] = ix if ix is not None else 0.0
+        tout.zero_()
+        tout.view(B, HW, -1)[..., :C + 1] = igy      # J a (tangent) = d<a, J^T gy>/d gy
+
+    # -- losses / optimizer -------------------------------------------------
+    def bce(self, logits, target, w, loss, u, h):
+        lv = logits.reshape(-1)
+        B = lv.numel()
+        s = torch.sigmoid(lv)
+        if target:
+            loss += w * F.softplus(-lv).mean()
+            if u is not None:
+                u.copy_(-w * (1 - s) / B)
+        else:
+            loss += w * F.softplus(lv).mean()
+            if u is not None:
+                u.copy_(w * s / B)
+        if h is not None:
+            h.copy_(w * s * (1 - s) / B)
+
+    def r1_penalty(self, g, B, r1, gbar):
+        r1 += 0.5 * (g * g).sum() / B
+        gbar.copy_(g / B)
+
+    def gp_interp(self, xr, xf, eps, out):
+        e = eps.view(-1, 1, 1, 1)
+        out.copy_(e * xr + (1 - e) * xf)
+
+    def gp_penalty(self, g, w, gp, norms, gbar):
+        B = g.shape[0]
+        n = g.reshape(B, -1).norm(dim=1)
+        norms.copy_(n * n)
+        gp += w * ((n - 1) ** 2).sum()
+        gbar.copy_((w * 2 * (n - 1) / n).view(B, *([1] * (g.dim() - 1))) * g)
+
+    def mul_add(self, x, y, z, out):
+        out.copy_(x + y * z)
+
+    def adam(self, p, g, m, v, *, lr, beta1, beta2, eps, step):
+        m.lerp_(g, 1 - beta1)
+        v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        bc1 = 1 - beta1 ** step
+        bc2 = 1 - beta2 ** step
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-lr / bc1)
+
+    def randn(self, out, seed, offset):
+        gen = torch.Generator().manual_seed(int(seed) * 1000003 + int(offset))
+        out.copy_(torch.randn(out.shape, generator=gen))
+
+    def cast(self, x, y):
+        y.copy_(x)
