@@ -1,0 +1,240 @@
+"""Benchmark: images/sec of the full PGGAN G+D+R1 training step (BASELINE.json metric).
+
+Workload (BASELINE configs[4] / SURVEY §8(d) C5): 1024x1024 stage (s=8), paper
+depths [512,512,512,512,256,128,64,32,16], batch 4 per GPU, alpha = 1, R1
+penalty, both Adam steps, bf16 storage with fp32 accumulation.  Synthetic data:
+reals U[-1,1) resident in HBM, latents drawn on the GPU by the pg_randn kernel,
+random-init weights (reference init: W ~ N(0,1), b = 0).
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+         (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+One process per GPU; gradients all-reduced (mean) over RCCL before each Adam step.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec (G+D+GP step) at 1024×1024 bs=4/GPU, 1/2/4/8 MI355X"
+PAPER_DEPTHS = [512, 512, 512, 512, 256, 128, 64, 32, 16]
+# dense peaks, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--stage", type=int, default=8)
+    p.add_argument("--batch", type=int, default=4)
+    p.add_argument("--alpha", type=float, default=1.0)
+    p.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-kernel-events", action="store_true")
+    return p.parse_args()
+
+
+class KernelTimer:
+    """HIP events around every conv launch (fwd/dgrad/tangent kernel and wgrad kernel),
+    recorded on the stream the kernels run on; FLOPs are the algorithmic MAC count x2
+    of the logical channels."""
+
+    def __init__(self, ops):
+        self.rec = {"conv3x3": [], "wgrad3x3": []}
+        self.on = False
+        f_conv, f_wg = ops.conv3x3, ops.conv_wgrad
+
+        def conv3x3(x, wpk, y, **kw):
+            if not self.on:
+                return f_conv(x, wpk, y, **kw)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f_conv(x, wpk, y, **kw)
+            b.record()
+            fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
+            self.rec["conv3x3"].append((a, b, fl))
+
+        def conv_wgrad(x, gz, dw, **kw):
+            if not self.on:
+                return f_wg(x, gz, dw, **kw)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            f_wg(x, gz, dw, **kw)
+            b.record()
+            fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
+            self.rec["wgrad3x3"].append((a, b, fl))
+
+        ops.conv3x3, ops.conv_wgrad = conv3x3, conv_wgrad
+
+    def summary(self):
+        out = {}
+        for k, lst in self.rec.items():
+            if not lst:
+                continue
+            ms = sum(a.elapsed_time(b) for a, b, _ in lst)
+            fl = sum(f for _, _, f in lst)
+            out[k] = dict(launches=len(lst), total_ms=ms, avg_us=1e3 * ms / len(lst),
+                          flops=fl, tflops=fl / (ms * 1e-3) / 1e12)
+        return out
+
+
+def init_params(E, depths, s, device, rank_seed):
+    gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
+    gen = torch.Generator().manual_seed(1234)   # same init on every rank (then broadcast)
+    init = lambda sh: {k: (torch.randn(v, generator=gen) if k.endswith("weight")
+                           else torch.zeros(v)) for k, v in sh}
+    fpG = E.FlatParams(gsh, E.dead_params("G", s), device, init(gsh))
+    fpD = E.FlatParams(dsh, E.dead_params("D", s), device, init(dsh))
+    return fpG, fpD
+
+
+def cpu_baseline(args, steps=1):
+    """The CPU oracle (fp32 restatement of the reference step, pinned to the reference's
+    golden vectors) on the host cores: one train_step at the same workload."""
+    from oracle import pggan_oracle as O
+    torch.set_num_threads(args.cpu_threads)
+    s, B = args.stage, args.batch
+    depths = PAPER_DEPTHS
+    gen = torch.Generator().manual_seed(7)
+    PG = {k: (torch.randn(v, generator=gen) if k.endswith("weight") else torch.zeros(v))
+          for k, v in O.g_param_shapes(depths, s)}
+    PD = {k: (torch.randn(v, generator=gen) if k.endswith("weight") else torch.zeros(v))
+          for k, v in O.d_param_shapes(depths, s)}
+    R = 4 * 2 ** s
+    real = torch.rand(B, 3, R, R, generator=gen) * 2 - 1
+    optG, optD = O.AdamState(1e-4), O.AdamState(1e-5)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        z1 = torch.randn(B, 512, generator=gen)
+        z2 = torch.randn(B, 512, generator=gen)
+        O.train_step(PG, PD, optG, optD, real, z1, z2, s, args.alpha, args.alpha)
+    dt = time.perf_counter() - t0
+    return dict(value=B * steps / dt, unit="images/sec", cores=args.cpu_threads, kind="port",
+                sample=f"{steps} oracle train_step at {R}x{R}, batch {B}, alpha {args.alpha} "
+                       f"(fp32, torch CPU, {args.cpu_threads} threads): {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from pggan_amd import _lib
+    from pggan_amd import engine as E
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    ops = _lib.HipOps(dtype)
+    timer = None if args.no_kernel_events else KernelTimer(ops)
+    s, B = args.stage, args.batch
+    depths = PAPER_DEPTHS
+    R = 4 * 2 ** s
+    fpG, fpD = init_params(E, depths, s, dev, rank)
+    if world > 1:   # replaces DDP's constructor-time broadcast (lib/model.py:78-79)
+        dist.broadcast(fpG.flat, 0)
+        dist.broadcast(fpD.flat, 0)
+    eng = E.StepEngine(ops, depths, s, B, dev)
+    eng.bind(fpG, fpD, E.Hyper())
+    gen = torch.Generator(device=dev).manual_seed(1000 * rank)
+    real = torch.rand(B, 3, R, R, device=dev, generator=gen) * 2 - 1
+    z = torch.empty(2, B, 512, device=dev)
+
+    def hook(net, g):
+        if world > 1:
+            dist.all_reduce(g)
+            g.mul_(1.0 / world)
+
+    step_no = [0]
+
+    def step():
+        ops.randn(z, 1000 * rank + 17, step_no[0] * z.numel())
+        step_no[0] += 1
+        eng.train_step(real, z[0], z[1], args.alpha, args.alpha, grad_hook=hook)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if timer:
+        timer.on = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if timer:
+        timer.on = False
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    assert torch.isfinite(eng.loss).all(), "non-finite loss"
+    ksum = timer.summary() if timer else {}
+
+    if rank == 0:
+        roof = None
+        if ksum:
+            dom = max(ksum, key=lambda k: ksum[k]["total_ms"])
+            kd = ksum[dom]
+            peak_key = "f32" if (dom == "wgrad3x3" or args.dtype == "f32") else "bf16"
+            peak = PEAK_TFLOPS[peak_key]
+            roof = dict(bound="mfma", kernel=dom, achieved=round(kd["tflops"], 2), peak=peak,
+                        unit="TFLOP/s", frac=round(kd["tflops"] / peak, 4), traffic=None,
+                        launches_per_step=kd["launches"] // args.steps,
+                        avg_launch_us=round(kd["avg_us"], 2),
+                        kernels={k: dict(total_ms_per_step=round(v["total_ms"] / args.steps, 3),
+                                         tflops=round(v["tflops"], 2),
+                                         launches_per_step=v["launches"] // args.steps)
+                                 for k, v in ksum.items()})
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            cpu = cpu_baseline(args)
+        line = {
+            "metric": METRIC,
+            "value": round(B * world * args.steps / dt, 3),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (U[-1,1) reals resident in HBM, N(0,1) latents on GPU, "
+                    "random-init weights)",
+            "config": {"workload": f"C5 G+D+R1 train_step, stage {s} ({R}x{R}), batch {B}/GPU, "
+                                   f"alpha {args.alpha}, depths {depths}",
+                       "global_batch": B * world, "resolution": R,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,381 @@
+"""ProgressiveGAN with the reference plugin interface (lib/model.py:8-138,
+pggan/model.py:11-265) running the MI355X step engine.
+
+Same method names, return values and schedule semantics as the reference:
+`initialize_models`, `set_multi_GPU`, `set_optimizers`, `set_dataset`,
+`set_data_iterator`, `set_loss_collector`, `load_next_batch`, `train_step` ->
+`[img_real, img_fake]`, `check_jump` / `change_scale` / `change_alpha` /
+`reset_alpha` / `reset_solver`, `save_checkpoint` / `load_checkpoint`
+(reference checkpoint file layout and dict keys), `save_image`, `validation`,
+`loss_collector`.  `G` and `D` are pggan_amd.nets modules whose parameters are
+views of the engine's flat fp32 buffers.
+
+Differences (deliberate):
+  * set_multi_GPU really all-reduces G and D gradients (mean over ranks) before
+    each Adam step; the reference discards its DDP wrapper (lib/model.py:78-79).
+  * latents are drawn on the GPU per rank (pg_randn) instead of the CPU RNG.
+"""
+from __future__ import annotations
+
+import glob
+import math
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import engine as E
+from .loss import WGANGPLoss
+from .nets import Discriminator, Generator
+
+
+class FlatAdam:
+    """torch.optim.Adam semantics (lib/model.py:95-97) over a net's flat buffers; the
+    state_dict() has torch.optim.Adam's layout so reference checkpoints interoperate."""
+
+    def __init__(self, fp: E.FlatParams, names, lr, betas, eps=1e-8):
+        self.fp, self.names = fp, list(names)
+        self.lr, self.betas, self.eps = lr, tuple(betas), eps
+        self.param_groups = [dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=0,
+                                  amsgrad=False, maximize=False, foreach=None,
+                                  capturable=False, differentiable=False, fused=None,
+                                  decoupled_weight_decay=False)]
+
+    def zero_grad(self, set_to_none=True):
+        self.fp.grad.zero_()
+
+    def state_dict(self):
+        st = {}
+        if self.fp.step > 0:
+            for i, n in enumerate(self.names):
+                if n in self.fp.dead:
+                    continue
+                st[i] = {"step": torch.tensor(float(self.fp.step)),
+                         "exp_avg": self.fp._view(self.fp.m, n).clone(),
+                         "exp_avg_sq": self.fp._view(self.fp.v, n).clone()}
+        pg = dict(self.param_groups[0])
+        pg["params"] = list(range(len(self.names)))
+        return {"state": st, "param_groups": [pg]}
+
+    def load_state_dict(self, sd):
+        steps = set()
+        for i, s in sd.get("state", {}).items():
+            n = self.names[int(i)]
+            self.fp._view(self.fp.m, n).copy_(s["exp_avg"])
+            self.fp._view(self.fp.v, n).copy_(s["exp_avg_sq"])
+            steps.add(int(float(s["step"])))
+        if steps:
+            self.fp.step = max(steps)
+        if sd.get("param_groups"):
+            g = sd["param_groups"][0]
+            self.lr, self.betas, self.eps = g["lr"], tuple(g["betas"]), g["eps"]
+
+
+class ImageFolderDataset:
+    """UnsupervisedDataset (lib/dataset.py:86-127) without torchvision: glob *.*g under
+    each root, resize to 2^(s+2), random horizontal flip, to [-1,1] NCHW fp32."""
+
+    def __init__(self, roots, scale_index=0, seed=0):
+        self.paths = []
+        for r in roots or []:
+            self.paths += glob.glob(f"{r}/*.*g")
+            for root, dirs, _ in os.walk(r):
+                for d in dirs:
+                    self.paths += glob.glob(f"{root}/{d}/*.*g")
+        self.size = 2 ** (scale_index + 2)
+        self.rng = np.random.default_rng(seed)
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        im = Image.open(self.paths[i]).convert("RGB").resize((self.size, self.size),
+                                                              Image.BILINEAR)
+        a = np.asarray(im, np.float32) / 127.5 - 1.0
+        if self.rng.random() < 0.5:
+            a = a[:, ::-1]
+        return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1)))
+
+
+class ProgressiveGAN:
+    """pggan/model.py:11-265."""
+
+    def __init__(self, args, gpu):
+        self.args = args
+        self.gpu = gpu
+        self.device = torch.device("cuda", gpu) if isinstance(gpu, int) else torch.device(gpu)
+        self.scale_index = 0
+        self.world, self.rank = 1, 0
+        self.dtype = torch.bfloat16 if getattr(args, "compute_dtype", "f32") == "bf16" \
+            else torch.float32
+        self.hyper = E.Hyper(lr_G=args.lr_G, lr_D=args.lr_D, beta1=float(args.beta1),
+                             beta2=float(args.beta2), W_adv=float(getattr(args, "W_adv", 1) or 0),
+                             slope_cfg=float(getattr(args, "LReLU_slope", 0.2)),
+                             gp_mode=getattr(args, "gp_mode", "r1"),
+                             W_gp=float(getattr(args, "W_gp", 10)))
+        self._engines = {}
+        self._rng_step = 0
+        self.global_step = 0
+        self.alpha_index = 0
+        self.alpha_jump_value = 0
+        self.next_alpha_jump_step = 0
+        self.next_scale_jump_step = 0
+        self.train_dataset = None
+        self.synthetic = None
+
+    # ------------------------------------------------------------------ models
+    def initialize_models(self):
+        a = self.args
+        self.G = Generator(a.latent_dim, a.depths[0], a.init_bias_to_zero, a.LReLU_slope,
+                           a.apply_pixel_norm, a.generator_last_activation, a.output_dim,
+                           a.equalized_lr).to(self.device)
+        self.D = Discriminator(a.depths[0], a.init_bias_to_zero, a.LReLU_slope,
+                               a.decision_layer_size, a.apply_minibatch_norm, a.input_dim,
+                               a.equalized_lr).to(self.device)
+        self.G.compute_dtype = self.dtype
+        self.D.compute_dtype = self.dtype
+        self.G.train()
+        self.D.train()
+
+    def set_multi_GPU(self):
+        """lib/model.py:74-79 + lib/utils.py:78-83, but with a working gradient all-reduce:
+        one process per GPU, RCCL, initial parameter broadcast from rank 0."""
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "3456")
+            dist.init_process_group("nccl", rank=int(os.environ.get("RANK", self.gpu)),
+                                    world_size=int(os.environ.get("WORLD_SIZE",
+                                                                  self.args.gpu_num)))
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self._broadcast_params()
+
+    def _broadcast_params(self):
+        if self.world > 1:
+            for net in (self.G, self.D):
+                for p in net.parameters():
+                    dist.broadcast(p.data, 0)
+
+    def _flat(self, net, which):
+        shapes = [(n, tuple(p.shape)) for n, p in net.named_parameters()]
+        init = {n: p.detach() for n, p in net.named_parameters()}
+        fp = E.FlatParams(shapes, E.dead_params(which, self.scale_index), self.device, init)
+        for n, p in net.named_parameters():
+            p.data = fp.views[n]
+            p.grad = fp.gviews[n]
+        return fp
+
+    def set_optimizers(self):
+        """lib/model.py:95-97: fresh Adam(lr, betas) for G and D (moments reset)."""
+        a = self.args
+        self.fpG, self.fpD = self._flat(self.G, "G"), self._flat(self.D, "D")
+        self.opt_G = FlatAdam(self.fpG, [n for n, _ in self.G.named_parameters()], a.lr_G,
+                              (float(a.beta1), float(a.beta2)))
+        self.opt_D = FlatAdam(self.fpD, [n for n, _ in self.D.named_parameters()], a.lr_D,
+                              (float(a.beta1), float(a.beta2)))
+
+    # ------------------------------------------------------------------ data
+    def set_dataset(self):
+        """pggan/model.py:118-126; falls back to a resident synthetic batch (the benchmark
+        setting) when no dataset root exists."""
+        roots = [r for r in (getattr(self.args, "dataset_root_list", None) or []) if os.path.isdir(r)]
+        ds = ImageFolderDataset(roots, self.scale_index, seed=self.rank)
+        if len(ds) == 0:
+            self.train_dataset = None
+            R = 4 * 2 ** self.scale_index
+            g = torch.Generator(device=self.device).manual_seed(1000 * self.rank)
+            self.synthetic = torch.rand(self.args.batch_per_gpu, 3, R, R, device=self.device,
+                                        generator=g) * 2 - 1
+        else:
+            n_train = round(len(ds) * 0.7)
+            perm = np.random.default_rng(0).permutation(len(ds))
+            ds.paths = [ds.paths[i] for i in perm[:n_train]]
+            self.train_dataset = ds
+
+    def set_data_iterator(self):
+        """lib/model.py:44-52: per-rank shard of a shuffled index order (DistributedSampler)."""
+        self._order, self._pos = None, 0
+        if self.train_dataset is not None:
+            n = len(self.train_dataset)
+            idx = np.arange(n)[self.rank::self.world]
+            self._order = idx
+
+    def load_next_batch(self):
+        """pggan/model.py:104-115."""
+        if self.train_dataset is None:
+            return self.synthetic
+        B = self.args.batch_per_gpu
+        if self._pos + B > len(self._order):
+            self._pos = 0
+        items = [self.train_dataset[int(i)] for i in self._order[self._pos:self._pos + B]]
+        self._pos += B
+        return torch.stack(items).to(self.device, non_blocking=True)
+
+    def set_loss_collector(self):
+        self._loss_collector = WGANGPLoss(self.args)
+
+    @property
+    def loss_collector(self):
+        return self._loss_collector
+
+    def set_validation(self):
+        pass
+
+    def validation(self, *args):
+        pass
+
+    # ------------------------------------------------------------------ step
+    def _engine(self, B):
+        key = (self.scale_index, B)
+        if key not in self._engines:
+            from . import _lib
+            self._engines = {}   # one stage at a time: free the previous stage's buffers
+            eng = E.StepEngine(_lib.HipOps(self.dtype), self.args.depths, self.scale_index, B,
+                               self.device, self.args.latent_dim)
+            self._engines[key] = eng
+        eng = self._engines[key]
+        eng.bind(self.fpG, self.fpD, self.hyper)
+        return eng
+
+    def _grad_hook(self, net, g):
+        if self.world > 1:
+            dist.all_reduce(g)
+            g.mul_(1.0 / self.world)
+
+    def train_step(self):
+        """pggan/model.py:206-255; returns [img_real, img_fake]."""
+        img_real = self.load_next_batch()
+        B = img_real.shape[0]
+        eng = self._engine(B)
+        self.hyper.lr_G, self.hyper.lr_D = self.opt_G.lr, self.opt_D.lr
+        z = getattr(self, "_z", None)
+        if z is None or z.shape[1] != B:
+            self._z = z = torch.empty(2, B, self.args.latent_dim, device=self.device)
+        eng.ops.randn(z, 1000 * self.rank + 17, self._rng_step * z.numel())
+        self._rng_step += 1
+        gp_eps = None
+        if self.hyper.gp_mode != "r1":
+            gp_eps = torch.rand(B, 1, device=self.device)
+        img_real, _, img_fake = eng.train_step(img_real, z[0], z[1], float(self.G.alpha),
+                                               float(self.D.alpha), grad_hook=self._grad_hook,
+                                               gp_eps=gp_eps)
+        self.loss_collector.attach(eng.loss, self.hyper.gp_mode)
+        return [img_real, img_fake]
+
+    # ------------------------------------------------------------------ schedule
+    def reset_solver(self):
+        """pggan/model.py:131-139."""
+        self.set_dataset()
+        self.set_data_iterator()
+        self.set_optimizers()
+
+    def reset_alpha(self, global_step):
+        """pggan/model.py:141-156."""
+        self.G.alpha = 0
+        self.D.alpha = 0
+        self.alpha_index = 0
+        self.next_alpha_jump_step = global_step + self.args.alpha_jump_start[self.scale_index]
+        self.alpha_jump_value = 1 / self.args.alpha_jump_Ntimes[self.scale_index]
+        if getattr(self.args, "isMaster", False):
+            print("alpha and alpha_index are initialized to 0")
+            print(f"next_alpha_jump_step is set to {self.next_alpha_jump_step}")
+            print(f"alpha_jump_value is set to {self.alpha_jump_value}")
+
+    def change_scale(self, global_step):
+        """pggan/model.py:158-174: add a block to G and D, fresh solver, reset alpha."""
+        self.scale_index += 1
+        self.next_scale_jump_step += self.args.max_step_at_scale[self.scale_index]
+        self.G.add_block(self.args.depths[self.scale_index])
+        self.D.add_block(self.args.depths[self.scale_index])
+        self._broadcast_params()
+        self.reset_solver()
+        self.reset_alpha(global_step)
+        if getattr(self.args, "isMaster", False):
+            print(f"\nNOW global_step is {global_step}")
+            print(f"scale_index is updated to {self.scale_index}")
+            print(f"next_scale_jump_step is {self.next_scale_jump_step}")
+
+    def change_alpha(self, global_step):
+        """pggan/model.py:176-194 (alpha rounded to 4 d.p.)."""
+        self.alpha_index += 1
+        self.G.alpha += self.alpha_jump_value
+        self.D.alpha += self.alpha_jump_value
+        self.G.alpha = round(self.G.alpha, 4)
+        self.D.alpha = round(self.D.alpha, 4)
+        if self.alpha_index == self.args.alpha_jump_Ntimes[self.scale_index]:
+            self.next_alpha_jump_step = 0
+        else:
+            self.next_alpha_jump_step = global_step + self.args.alpha_jump_interval[self.scale_index]
+        if getattr(self.args, "isMaster", False):
+            print(f"\nNOW global_step is {global_step}")
+            print(f"alpha_index is updated to {self.alpha_index}")
+            print(f"next_alpha_jump_step is {self.next_alpha_jump_step}")
+            print(f"alpha is now {self.G.alpha}")
+
+    def check_jump(self, global_step):
+        """pggan/model.py:196-204."""
+        if self.next_scale_jump_step == global_step:
+            self.change_scale(global_step)
+        if self.next_alpha_jump_step == global_step:
+            self.change_alpha(global_step)
+
+    # ------------------------------------------------------------------ persistence
+    def _ckpt_dict(self, global_step):
+        return {"args": dict(self.args.__dict__), "global_step": global_step,
+                "alpha_G": self.G.alpha, "alpha_D": self.D.alpha,
+                "alpha_index": self.alpha_index, "alpha_jump_value": self.alpha_jump_value,
+                "next_alpha_jump_step": self.next_alpha_jump_step,
+                "scale_index": self.scale_index,
+                "next_scale_jump_step": self.next_scale_jump_step}
+
+    def save_checkpoint(self, global_step):
+        """pggan/model.py:50-67 + lib/checkpoint.py:22-34 (same paths and keys)."""
+        from . import checkpoint
+        base = self._ckpt_dict(global_step)
+        checkpoint.save_checkpoint(self.G, self.opt_G, "G", dict(base))
+        checkpoint.save_checkpoint(self.D, self.opt_D, "D", dict(base))
+
+    def load_checkpoint(self):
+        """pggan/model.py:70-101: restore schedule scalars, re-add blocks, fresh solver, then
+        load model (strict=False) and optimizer state."""
+        from . import checkpoint
+        Gd = checkpoint.load_checkpoint(self.args, "G", self.device)
+        Dd = checkpoint.load_checkpoint(self.args, "D", self.device)
+        if not Gd or not Dd:
+            raise RuntimeError("checkpoint not found")
+        for k, v in Gd["args"].items():
+            setattr(self.args, k, v) if not hasattr(self.args, "__setitem__") else \
+                self.args.__setitem__(k, v)
+        self.global_step = Gd["global_step"]
+        self.alpha_index = Gd["alpha_index"]
+        self.alpha_jump_value = Gd["alpha_jump_value"]
+        self.next_alpha_jump_step = Gd["next_alpha_jump_step"]
+        self.next_scale_jump_step = Gd["next_scale_jump_step"]
+        target = Gd["scale_index"]
+        # the reference re-adds blocks with depths[index] for index in range(scale_index)
+        # (pggan/model.py:89-93); it builds a model whose depth list is depths[0..s]
+        while self.scale_index < target:
+            self.scale_index += 1
+            self.G.add_block(self.args.depths[self.scale_index])
+            self.D.add_block(self.args.depths[self.scale_index])
+        self.reset_solver()
+        self.G.alpha = Gd["alpha_G"]
+        self.D.alpha = Gd["alpha_D"]
+        self.G.load_state_dict(Gd["model"], strict=False)
+        self.D.load_state_dict(Dd["model"], strict=False)
+        self.opt_G.load_state_dict(Gd["optimizer"])
+        self.opt_D.load_state_dict(Dd["optimizer"])
+
+    def save_image(self, images, step):
+        """lib/utils.py:86-103: grid of up to 8 images per row, rows = tensors, [-1,1] ->
+        [0,255], written to {save_root}/{run_id}/imgs/e{step}.jpg."""
+        from PIL import Image
+        rows = []
+        for t in images:
+            t = t[:8].detach().float().cpu().clamp(-1, 1) * 0.5 + 0.5
+            rows.append(torch.cat(list(t), dim=2))
+        grid = torch.cat(rows, dim=1).permute(1, 2, 0).numpy()
+        d = f"{self.args.save_root}/{self.args.run_id}/imgs"
+        os.makedirs(d, exist_ok=True)
+        Image.fromarray((grid * 255).astype(np.uint8)).save(f"{d}/e{step}.jpg")

@@ -1,0 +1,193 @@
+"""Generator / Discriminator modules with the reference's Python surface
+(pggan/nets.py:10-276): constructor arguments, `add_block(depth)`, float
+attribute `alpha`, `forward(z)` / `forward(x, get_feature=False)`, and the exact
+`state_dict` keys of the reference (``blocks.{i}.block.{0,3}.module.weight`` ...),
+so reference checkpoints load unchanged.
+
+Compute goes through the HIP kernels (pggan_amd.engine).  forward() is the
+inference / sampling path (no autograd graph); training uses the hand-scheduled
+step in ProgressiveGAN.train_step.  Non-default architecture switches that the
+reference exposes but never uses (equalized_lr=False, apply_pixel_norm=False,
+last_activation, LReLU_slope on blocks) raise NotImplementedError.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import engine as E
+
+
+class _Param(nn.Module):
+    """Stands in for ConstrainedLayer.module (lib/layers.py:48): holds weight/bias."""
+
+    def __init__(self, wshape, bshape, init_bias_to_zero=True):
+        super().__init__()
+        self.weight = nn.Parameter(torch.randn(*wshape))            # lib/layers.py:54
+        b = torch.zeros(*bshape) if init_bias_to_zero else torch.randn(*bshape) * 0.0
+        self.bias = nn.Parameter(b)                                  # lib/layers.py:51-52
+
+
+class _Eq(nn.Module):
+    def __init__(self, wshape, bshape, init_bias_to_zero=True):
+        super().__init__()
+        self.module = _Param(wshape, bshape, init_bias_to_zero)
+
+
+class _Seq(nn.Module):
+    """A parameter container whose children are indexed like nn.Sequential."""
+
+    def __init__(self, entries):
+        super().__init__()
+        for i, m in entries:
+            self.add_module(str(i), m)
+
+
+class _GBlock(nn.Module):
+    def __init__(self, prev, new, is_first, ibz):
+        super().__init__()
+        if is_first:
+            self.block = _Seq([(0, _Eq((new, new, 3, 3), (new,), ibz))])
+        else:
+            self.block = _Seq([(0, _Eq((new, prev, 3, 3), (new,), ibz)),
+                               (3, _Eq((new, new, 3, 3), (new,), ibz))])
+
+
+class _DBlock(nn.Module):
+    def __init__(self, new, prev, ibz):
+        super().__init__()
+        self.block = _Seq([(0, _Eq((new, new, 3, 3), (new,), ibz)),
+                           (2, _Eq((prev, new, 3, 3), (prev,), ibz))])
+
+
+class _ToRGB(nn.Module):
+    def __init__(self, depth, out_dim, ibz):
+        super().__init__()
+        self.toRGB = _Eq((out_dim, depth, 1, 1), (out_dim,), ibz)
+
+
+class _FromRGB(nn.Module):
+    def __init__(self, in_dim, depth, ibz):
+        super().__init__()
+        self.fromRGB = _Eq((depth, in_dim, 1, 1), (depth,), ibz)
+
+
+class _MBBlock(nn.Module):
+    def __init__(self, depth, ibz):
+        super().__init__()
+        self.conv = _Eq((depth, depth + 1, 3, 3), (depth,), ibz)
+        self.linear = _Eq((depth, depth * 16), (depth,), ibz)
+
+
+_ENGINES = {}
+
+
+def _engine(ops_dtype, depths, s, B, device):
+    from . import _lib
+    key = (ops_dtype, tuple(depths), s, B, str(device))
+    if key not in _ENGINES:
+        eng = E.StepEngine(_lib.HipOps(ops_dtype), depths, s, B, device)
+        eng.hyper = E.Hyper()
+        _ENGINES[key] = eng
+    return _ENGINES[key]
+
+
+class Generator(nn.Module):
+    """pggan/nets.py:10-161."""
+
+    def __init__(self, latent_dim, first_depth, init_bias_to_zero=True, LReLU_slope=0.2,
+                 apply_pixel_norm=True, last_activation=None, output_dim=3, equalized_lr=True):
+        super().__init__()
+        if not equalized_lr or not apply_pixel_norm or last_activation is not None:
+            raise NotImplementedError("pggan_amd implements the reference's default G "
+                                      "(equalized_lr, pixel norm, no last activation)")
+        if output_dim != 3:
+            raise NotImplementedError("pggan_amd kernels produce RGB output")
+        self.latent_dim = latent_dim
+        self.first_depth = first_depth
+        self.init_bias_to_zero = init_bias_to_zero
+        self.LReLU_slope = LReLU_slope
+        self.output_dim = output_dim
+        self.block_depths = [first_depth]
+        self.blocks = nn.ModuleList()
+        self.toRGB_blocks = nn.ModuleList()
+        self.latent_format_layer = _Eq((16 * first_depth, latent_dim), (16 * first_depth,),
+                                       init_bias_to_zero)
+        self.first_block = _GBlock(first_depth, first_depth, True, init_bias_to_zero)
+        self.toRGB_blocks.append(_ToRGB(first_depth, output_dim, init_bias_to_zero))
+        self.alpha = 0
+        self.compute_dtype = torch.float32
+
+    def add_block(self, new_depth):
+        """pggan/nets.py:102-119."""
+        prev = self.block_depths[-1]
+        self.block_depths.append(new_depth)
+        dev = self.latent_format_layer.module.weight.device
+        self.blocks.append(_GBlock(prev, new_depth, False, self.init_bias_to_zero).to(dev))
+        self.toRGB_blocks.append(_ToRGB(new_depth, self.output_dim, self.init_bias_to_zero).to(dev))
+
+    @property
+    def scale_index(self):
+        return len(self.blocks)
+
+    def forward(self, x):
+        """pggan/nets.py:121-161 on the HIP kernels (no autograd graph)."""
+        s = self.scale_index
+        B = x.shape[0]
+        eng = _engine(self.compute_dtype, self.block_depths, s, B, x.device)
+        eng.hyper.slope_cfg = self.LReLU_slope
+        P = dict(self.named_parameters())
+        with torch.no_grad():
+            eng.pack("G", P)
+            img = eng.g_forward(P, x.reshape(B, -1).float(), float(self.alpha))
+        return img.clone()
+
+
+class Discriminator(nn.Module):
+    """pggan/nets.py:164-276."""
+
+    def __init__(self, last_depth, init_bias_to_zero=True, LReLU_slope=0.2, decision_layer_size=1,
+                 apply_minibatch_norm=False, input_dim=3, equalized_lr=True):
+        super().__init__()
+        if not equalized_lr or not apply_minibatch_norm or decision_layer_size != 1:
+            raise NotImplementedError("pggan_amd implements the reference's configured D "
+                                      "(equalized_lr, minibatch stddev, one logit)")
+        if input_dim != 3:
+            raise NotImplementedError("pggan_amd kernels consume RGB input")
+        self.init_bias_to_zero = init_bias_to_zero
+        self.input_dim = input_dim
+        self.depths = [last_depth]
+        self.blocks = nn.ModuleList()
+        self.fromRGB_blocks = nn.ModuleList()
+        self.mergeLayers = nn.ModuleList()
+        self.decision_layer = _Eq((decision_layer_size, last_depth), (decision_layer_size,),
+                                  init_bias_to_zero)
+        self.minibatch_normalization_block = _MBBlock(last_depth, init_bias_to_zero)
+        self.fromRGB_blocks.append(_FromRGB(input_dim, last_depth, init_bias_to_zero))
+        self.alpha = 0
+        self.compute_dtype = torch.float32
+
+    def add_block(self, new_depth):
+        """pggan/nets.py:227-239."""
+        prev = self.depths[-1]
+        self.depths.append(new_depth)
+        dev = self.decision_layer.module.weight.device
+        self.blocks.append(_DBlock(new_depth, prev, self.init_bias_to_zero).to(dev))
+        self.fromRGB_blocks.append(_FromRGB(self.input_dim, new_depth, self.init_bias_to_zero).to(dev))
+
+    @property
+    def scale_index(self):
+        return len(self.blocks)
+
+    def forward(self, x, get_feature=False):
+        """pggan/nets.py:248-276 on the HIP kernels (no autograd graph)."""
+        s = self.scale_index
+        B = x.shape[0]
+        eng = _engine(self.compute_dtype, self.depths, s, B, x.device)
+        P = dict(self.named_parameters())
+        with torch.no_grad():
+            eng.pack("D", P)
+            out = eng.d_forward(P, x.float().contiguous(), float(self.alpha)).clone()
+        if not get_feature:
+            return out
+        return out, eng.dd["l1"].float().clone()

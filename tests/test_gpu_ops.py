@@ -1,0 +1,324 @@
+"""Kernel-level parity: every HIP entry point (via pggan_amd._lib.HipOps) against the
+CPU test double on identical random inputs.  fp32 mode must agree to ~1e-5
+(exact-fp32 MFMA, different summation order); bf16 mode to bf16 rounding."""
+import itertools
+
+import pytest
+import torch
+
+from cpu_ops import CpuOps, cinp, r16
+from golden_utils import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+L = None
+
+
+def lib():
+    global L
+    if L is None:
+        from pggan_amd import _lib
+        L = _lib
+    return L
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def ops_pair(dtype):
+    return lib().HipOps(dtype), CpuOps()
+
+
+def cmp(a_gpu, b_cpu, tol, what):
+    a = a_gpu.float().cpu().numpy()
+    b = b_cpu.float().numpy()
+    e = rel_l2(a, b)
+    assert e <= tol, f"{what}: rel err {e:.3e} > {tol:.1e}"
+
+
+def tol_for(dtype, base=2e-5):
+    return base if dtype == torch.float32 else 2e-2
+
+
+def q(t, dtype):
+    """round a CPU fp32 tensor through the storage dtype (so both sides see the same data)"""
+    return t.to(dtype).float()
+
+
+CONV_CASES = [
+    # (B, H, cin, cout, flags)
+    (2, 8, 32, 32, ("bias", "lrelu")),
+    (3, 4, 64, 64, ("bias", "lrelu")),          # tiny images, several per tile, ragged B
+    (2, 16, 16, 16, ("ups", "bias", "lrelu")),
+    (1, 32, 8, 8, ("bias", "lrelu")),
+    (2, 16, 32, 64, ("bias", "lrelu", "pool")),
+    (2, 32, 64, 32, ("mask",)),
+    (2, 8, 128, 48, ("accum",)),
+    (1, 64, 16, 32, ("pool", "accum")),
+    (4, 4, 33, 32, ("bias", "lrelu")),          # mbstd-style padded cin (33 -> 64)
+    (2, 8, 32, 20, ("bias",)),                  # cout not a multiple of 16
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv3x3_fwd(case, dtype):
+    B, H, cin, cout, fl = case
+    _L = lib()
+    hip, cpu = ops_pair(dtype)
+    flags = 0
+    for f, v in (("ups", _L.CONV_UPS_IN), ("bias", _L.CONV_BIAS), ("lrelu", _L.CONV_LRELU),
+                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM)):
+        if f in fl:
+            flags |= v
+    Hin = H // 2 if "ups" in fl else H
+    xcs = cinp(cin)
+    x = q(rnd(B, Hin, Hin, xcs, seed=1), dtype)
+    x[..., cin:] = 0
+    w = rnd(cout, cin, 3, 3, seed=2)
+    bias = rnd(cout, seed=3) * 0.1
+    Ho = H // 2 if "pool" in fl else H
+    ycs = cout + 4
+    y0 = q(rnd(B, Ho, Ho, ycs, seed=4), dtype)
+    aux = q(rnd(B, H, H, cout, seed=5), dtype)
+    scale = 0.05
+    outs = []
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        wp = torch.zeros(ops.packed_elems(0, cout, cin), dtype=dtype if dev == "cuda" else torch.float32,
+                         device=dev)
+        ops.conv_pack(0, w.to(dev), scale, wp)
+        y = y0.to(dev).to(wp.dtype).clone()
+        y2 = torch.zeros(B, H, H, cout, dtype=wp.dtype, device=dev) if "pool" in fl else None
+        ops.conv3x3(x.to(dev).to(wp.dtype), wp, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
+                    slope=0.2, out_scale=0.25 if "pool" in fl else 1.0,
+                    bias=(bias * scale).to(dev), aux=aux.to(dev).to(wp.dtype), y2=y2)
+        outs.append((y, y2))
+    cmp(outs[0][0], outs[1][0], tol_for(dtype), "conv y")
+    if outs[0][1] is not None:
+        cmp(outs[0][1], outs[1][1], tol_for(dtype), "conv y2")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 8, 32, 48), (2, 16, 16, 16), (3, 4, 513, 512), (1, 32, 8, 8)])
+def test_conv3x3_dgrad_pack(case, dtype):
+    """dgrad = conv with the PACK_DGRAD layout (flipped / transposed weights)."""
+    B, H, cin, cout = case
+    hip, cpu = ops_pair(dtype)
+    w = rnd(cout, cin, 3, 3, seed=7)
+    gz = q(rnd(B, H, H, cinp(cout), seed=8), dtype)
+    gz[..., cout:] = 0
+    outs = []
+    cout_d = (cin + 3) // 4 * 4
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        wp = torch.zeros(ops.packed_elems(1, cout, cin), dtype=dt, device=dev)
+        ops.conv_pack(1, w.to(dev), 0.1, wp)
+        y = torch.zeros(B, H, H, cinp(cin), dtype=dt, device=dev)
+        ops.conv3x3(gz.to(dev).to(dt), wp, y, B=B, H=H, W=H, cin=cout, cout=cout_d, flags=0)
+        outs.append(y)
+    cmp(outs[0], outs[1], tol_for(dtype), "dgrad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, False),
+                                  (1, 64, 8, 8, False), (2, 32, 64, 32, True)])
+def test_conv3x3_wgrad(case, dtype):
+    B, H, cin, cout, ups = case
+    hip, cpu = ops_pair(dtype)
+    Hin = H // 2 if ups else H
+    x = q(rnd(B, Hin, Hin, cinp(cin), seed=11), dtype)
+    gz = q(rnd(B, H, H, cout, seed=12), dtype)
+    outs = []
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        dw = torch.full((cout, cin, 3, 3), 0.5, device=dev)
+        ops.conv_wgrad(x.to(dev).to(dt), gz.to(dev).to(dt), dw, B=B, H=H, W=H, cin=cin, cout=cout,
+                       ups=ups, scale=0.3)
+        outs.append(dw)
+    cmp(outs[0], outs[1], 2e-5 if dtype == torch.float32 else 1e-4, "wgrad")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_elementwise_ops(dtype):
+    hip, cpu = ops_pair(dtype)
+    B, H, C = 2, 8, 32
+    x = q(rnd(B, H, H, C, seed=21), dtype)
+    g = q(rnd(B, H // 2, H // 2, C, seed=22), dtype)
+    y = q(rnd(B, H, H, C, seed=23), dtype)
+    tol = tol_for(dtype, 1e-6)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        X, G, Y = x.to(dev).to(dt), g.to(dev).to(dt), y.to(dev).to(dt)
+        r = {}
+        r["pn"] = torch.zeros_like(X); ops.pixnorm(X, r["pn"], C)
+        r["pnb"] = torch.zeros_like(X); ops.pixnorm_lrelu_bwd(X, Y, r["pnb"], C, 0.2)
+        r["um"] = torch.zeros_like(X)
+        ops.unpool_mask(G, Y, r["um"], B=B, H=H, W=H, C=C, scale=0.25, slope=0.2, ups=True)
+        r["ap"] = torch.zeros_like(G); ops.avgpool2(X, r["ap"], B=B, H=H, W=H, C=C)
+        r["bl"] = torch.zeros_like(X); ops.blend(0.3, X, 0.7, Y, r["bl"])
+        db = torch.zeros(C, device=dev); ops.bias_grad(X, db, C, 0.5); r["db"] = db
+        res[dev] = r
+    for k in res["cpu"]:
+        cmp(res["cuda"][k], res["cpu"][k], tol if k != "db" else 1e-5, k)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("s", [0, 2])
+def test_rgb_ops(dtype, s):
+    hip, cpu = ops_pair(dtype)
+    B, R, C, Cp = 2, 4 * 2 ** s, 16, 32
+    x = q(rnd(B, R, R, C, seed=31), dtype)
+    xp = q(rnd(B, R // 2, R // 2, Cp, seed=32), dtype)
+    w, b = rnd(3, C, 1, 1, seed=33), rnd(3, seed=34)
+    wp, bp = rnd(3, Cp, 1, 1, seed=35), rnd(3, seed=36)
+    gimg = rnd(B, 3, R, R, seed=37)
+    img = rnd(B, 3, R, R, seed=38)
+    fw, fb = rnd(C, 3, 1, 1, seed=39), rnd(C, seed=40)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        X, XP = x.to(dev).to(dt), xp.to(dev).to(dt)
+        kw = dict(xp=XP, wp=wp.to(dev), bp=bp.to(dev), cp=0.2, Cp=Cp, alpha=0.3) if s else {}
+        r = {"img": torch.zeros(B, 3, R, R, device=dev)}
+        ops.rgb_out(X, w.to(dev), b.to(dev), 0.35, r["img"], B=B, R=R, C=C, **kw)
+        r["gx"] = torch.zeros_like(X)
+        r["dw"] = torch.zeros(3, C, 1, 1, device=dev)
+        r["db"] = torch.zeros(3, device=dev)
+        kwb = {}
+        if s:
+            r["gxp"] = torch.zeros_like(XP)
+            r["dwp"] = torch.zeros(3, Cp, 1, 1, device=dev)
+            r["dbp"] = torch.zeros(3, device=dev)
+            kwb = dict(xp=XP, wp=wp.to(dev), cp=0.2, Cp=Cp, alpha=0.3, gxp=r["gxp"], dwp=r["dwp"],
+                       dbp=r["dbp"])
+        ops.rgb_out_bwd(X, w.to(dev), 0.35, gimg.to(dev), r["gx"], r["dw"], r["db"], B=B, R=R, C=C,
+                        **kwb)
+        for down in ((False, True) if s else (False,)):
+            Ro = R // 2 if down else R
+            yy = torch.zeros(B, Ro, Ro, C, dtype=dt, device=dev)
+            ops.from_rgb(img.to(dev), fw.to(dev), fb.to(dev), 0.8, yy, B=B, R=Ro, C=C, down=down)
+            r[f"fr{down}"] = yy
+            ty = torch.zeros_like(yy)
+            ops.from_rgb(img.to(dev), fw.to(dev), None, 0.8, ty, B=B, R=Ro, C=C, down=down,
+                         mask_y=yy)
+            r[f"ft{down}"] = ty
+            gi = torch.zeros(B, 3, R, R, device=dev)
+            dw_ = torch.zeros(C, 3, 1, 1, device=dev)
+            db_ = torch.zeros(C, device=dev)
+            ops.from_rgb_bwd(yy, fw.to(dev), 0.8, B=B, R=Ro, C=C, down=down, img=img.to(dev),
+                             gimg=gi, dw=dw_, db=db_)
+            r[f"fgi{down}"], r[f"fdw{down}"], r[f"fdb{down}"] = gi, dw_, db_
+        fo = torch.zeros_like(img.to(dev))
+        if s:
+            ops.img_fade(img.to(dev), 0.4, fo)
+        r["fade"] = fo
+        res[dev] = r
+    for k in res["cpu"]:
+        cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 2e-5), k)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B", [1, 4, 6, 16])
+def test_linear_mbstd_loss(dtype, B):
+    _L = lib()
+    hip, cpu = ops_pair(dtype)
+    C = 32
+    mcs = cinp(C + 1)
+    x = q(rnd(B, 4, 4, C, seed=51), dtype)
+    w = rnd(C, 16 * C, seed=52)
+    bb = rnd(C, seed=53)
+    wdec = rnd(1, C, seed=54)
+    aux = q(rnd(B, 4, 4, C, seed=55), dtype)
+    gy = q(rnd(B, 4, 4, mcs, seed=56), dtype)
+    a = q(rnd(B, 4, 4, C, seed=57), dtype)
+    z = rnd(B, 64, seed=58)
+    wf = rnd(16 * C, 64, seed=59)
+    logits = rnd(B, 1, seed=60)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        X, AUX, GY, A = (t.to(dev).to(dt) for t in (x, aux, gy, a))
+        r = {}
+        r["l1"] = torch.zeros(B, C, dtype=dt, device=dev)
+        ops.linear(X, w.to(dev), bb.to(dev), r["l1"], B=B,
+                   flags=_L.LIN_BIAS | _L.LIN_LRELU | _L.LIN_IN_CHW, scale=0.1)
+        r["out"] = torch.zeros(B, 1, device=dev)
+        ops.linear(r["l1"], wdec.to(dev), torch.zeros(1, device=dev), r["out"], B=B, flags=_L.LIN_BIAS,
+                   scale=0.2)
+        r["gl1"] = torch.zeros(B, C, dtype=dt, device=dev)
+        ops.linear_dgrad(r["out"], wdec.to(dev), r["gl1"], B=B, flags=_L.LIN_MASK, scale=0.2,
+                         aux=r["l1"])
+        r["gx"] = torch.zeros_like(X)
+        ops.linear_dgrad(r["gl1"], w.to(dev), r["gx"], B=B, flags=_L.LIN_IN_CHW | _L.LIN_MASK,
+                         scale=0.1, aux=AUX)
+        r["dw"] = torch.zeros_like(w.to(dev))
+        r["db"] = torch.zeros(C, device=dev)
+        ops.linear_wgrad(X, r["gl1"], r["dw"], r["db"], B=B, flags=_L.LIN_IN_CHW, scale=0.1)
+        r["f"] = torch.zeros(B, 4, 4, C, dtype=dt, device=dev)
+        ops.linear(z.to(dev), wf.to(dev), torch.zeros(16 * C, device=dev), r["f"], B=B,
+                   flags=_L.LIN_BIAS | _L.LIN_LRELU | _L.LIN_OUT_CHW, scale=0.3)
+        r["dwf"] = torch.zeros(16 * C, 64, device=dev)
+        ops.linear_wgrad(z.to(dev), r["f"], r["dwf"], None, B=B, flags=_L.LIN_OUT_CHW, scale=0.3)
+        r["m"] = torch.zeros(B, 4, 4, mcs, dtype=dt, device=dev)
+        ops.mbstd_fwd(X, r["m"], B=B, HW=16, C=C)
+        r["gm"] = torch.zeros_like(X)
+        ops.mbstd_bwd(X, GY, r["gm"], B=B, HW=16, C=C)
+        r["tout"] = torch.zeros(B, 4, 4, mcs, dtype=dt, device=dev)
+        r["inj"] = torch.zeros_like(X)
+        ops.mbstd_r1(X, A, GY, r["tout"], r["inj"], B=B, HW=16, C=C)
+        for tgt in (True, False):
+            lo = torch.zeros(1, device=dev)
+            u = torch.zeros(B, device=dev)
+            h = torch.zeros(B, device=dev)
+            ops.bce(logits.to(dev), tgt, 0.7, lo, u, h)
+            r[f"bce{tgt}"], r[f"u{tgt}"], r[f"h{tgt}"] = lo, u, h
+        gimg = logits.to(dev).view(B, 1, 1, 1).expand(B, 3, 4, 4).contiguous() * 1e-3
+        r1 = torch.zeros(1, device=dev)
+        gbar = torch.zeros_like(gimg)
+        ops.r1_penalty(gimg, B, r1, gbar)
+        r["r1"], r["gbar"] = r1, gbar
+        gp = torch.zeros(1, device=dev)
+        nrm = torch.zeros(B, device=dev)
+        gb2 = torch.zeros_like(gimg)
+        ops.gp_penalty(gimg, 10.0, gp, nrm, gb2)
+        r["gp"], r["gpbar"] = gp, gb2
+        res[dev] = r
+    for k in res["cpu"]:
+        tol = tol_for(dtype, 3e-5)
+        if k in ("inj", "tout") and dtype == torch.float32:
+            tol = 2e-4   # closed form vs autograd; includes 1/sigma^3 terms
+        cmp(res["cuda"][k], res["cpu"][k], tol, k)
+
+
+def test_adam_matches_torch():
+    hip, cpu = ops_pair(torch.float32)
+    n = 10000
+    p0, g1, g2 = rnd(n, seed=71), rnd(n, seed=72) * 1e-3, rnd(n, seed=73)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        p = p0.clone().to(dev)
+        m = torch.zeros(n, device=dev)
+        v = torch.zeros(n, device=dev)
+        for t, g in enumerate((g1, g2), start=1):
+            ops.adam(p, g.to(dev), m, v, lr=1e-4, beta1=0.0, beta2=0.99, eps=1e-8, step=t)
+        res[dev] = p
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.Adam([ref], lr=1e-4, betas=(0.0, 0.99), eps=1e-8)
+    for g in (g1, g2):
+        ref.grad = g.clone()
+        opt.step()
+    cmp(res["cuda"], ref.detach(), 1e-7, "adam vs torch.optim.Adam")
+    cmp(res["cpu"], ref.detach(), 1e-7, "cpu double vs torch.optim.Adam")
+
+
+def test_randn_moments():
+    hip = lib().HipOps(torch.float32)
+    z = torch.empty(1 << 20, device="cuda")
+    hip.randn(z, 1234, 0)
+    assert abs(z.mean().item()) < 5e-3 and abs(z.std().item() - 1) < 5e-3
+    z2 = torch.empty(1 << 20, device="cuda")
+    hip.randn(z2, 1234, 0)
+    assert torch.equal(z, z2)

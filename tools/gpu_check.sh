@@ -1,0 +1,34 @@
+#!/bin/bash
+# GPU-box check: each GPU step under its own time limit; stops at the first step that
+# ends other than pass (0) / test failures (1).  Logs under gpurun_out/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1; shift
+  local t=$1; shift
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    ops) run ops 900 python -m pytest tests/test_gpu_ops.py -q -x ;;
+    parity) run parity 1200 python -m pytest tests/test_gpu_parity.py -q ;;
+    gpu) run gpu 1500 python -m pytest tests -q -m gpu ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py --steps 5 --warmup 2 ;;
+    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
+    prof)
+      ROOT=$(pwd)
+      export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$ROOT/gpurun_out/prof" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 \
+          --cpu-baseline off --no-kernel-events ) > gpurun_out/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"; tail -n 3 gpurun_out/prof.log
+      if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
