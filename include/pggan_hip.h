@@ -69,9 +69,11 @@ int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw,
 int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                    const float* bias, const void* aux, void* y, void* y2, void* stream);
 /* weight gradient, accumulates: dw[o][c][ky][kx] += scale * sum_p gz[p][o] * x[p+tap][c]
- * (desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold PG_CONV_UPS_IN) */
+ * and, if db != NULL, the bias gradient db[o] += scale * sum_p gz[p][o] (fused: gz is read
+ * once).  desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold
+ * PG_CONV_UPS_IN.  bf16: cout and both channel strides must be multiples of 8. */
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, void* stream);
+                     float* dw, float* db, void* stream);
 /* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
                  void* stream);

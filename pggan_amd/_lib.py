@@ -43,7 +43,7 @@ _SIGS = {
     "pg_conv3x3_packed_elems": ([_I, _I, _I], _SZ),
     "pg_conv3x3_pack": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),
-    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP], _I),
+    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP], _I),
     "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
@@ -144,12 +144,12 @@ class HipOps:
         self._chk(self.lib.pg_conv3x3_fwd(self._dt(y), ctypes.byref(d), _p(x), _p(wpk), _p(bias),
                                           _p(aux), _p(y), _p(y2), self._s()), "conv3x3_fwd")
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale):
-        self._cuda(x, gz, dw)
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None):
+        self._cuda(x, gz, dw, db)
         d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0,
                      CONV_UPS_IN if ups else 0, 0.0, 1.0)
         self._chk(self.lib.pg_conv3x3_wgrad(self._dt(gz), ctypes.byref(d), _p(x), _p(gz), scale,
-                                            _p(dw), self._s()), "conv3x3_wgrad")
+                                            _p(dw), _p(db), self._s()), "conv3x3_wgrad")
 
     def bias_grad(self, g, db, C, scale):
         self._cuda(g, db)

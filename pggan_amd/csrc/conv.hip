@@ -39,6 +39,23 @@ struct ConvParams {
   int pixb, wrowb, halo_bytes;
 };
 
+int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
+
+struct TileCfg {
+  int BM, BN, NB, TH, TW;
+};
+
+TileCfg pick_tile(int H, int W, int BM, int BN) {
+  TileCfg t;
+  t.BM = BM;
+  t.BN = BN;
+  t.TW = W < 16 ? W : 16;
+  t.TH = BM / t.TW;
+  if (t.TH > H) t.TH = H;
+  t.NB = BM / (t.TH * t.TW);
+  return t;
+}
+
 template <typename T>
 struct Frag;
 
@@ -269,6 +286,7 @@ struct WgParams {
   const void* x;
   const void* gz;
   float* dw;
+  float* db;
   int B, H, W, Hin, Win;
   int cin, cout, x_cs, gz_cs;
   int ups;
@@ -294,6 +312,8 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
   f32x4_t acc[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) acc[q] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;   // bias gradient of output channel o0 + tid (c-tile 0 only)
+  const bool do_db = p.db && blockIdx.y == 0 && tid < WG_BO;
 
   const int t_begin = blockIdx.z * p.tiles_per_split;
   const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
@@ -329,6 +349,8 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
       hal[hp * WG_RS + ci] = v;
     }
     __syncthreads();
+    if (do_db)
+      for (int pm = 0; pm < WG_BP; ++pm) bsum += gzl[pm * WG_RS + tid];
     for (int k0 = 0; k0 < WG_BP; k0 += 4) {
       const int pm = k0 + g;
       const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
@@ -341,6 +363,7 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
       }
     }
   }
+  if (do_db && o0 + tid < p.cout) atomicAdd(p.db + o0 + tid, bsum * p.scale);
   // acc[tap][j]: row (o) = om + 4g + j, col (c) = cn + r
   const int c = cc0 + cn + r;
 #pragma unroll
@@ -352,6 +375,229 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
       for (int tap = 0; tap < 9; ++tap) atomicAdd(dst + tap, acc[tap][j] * p.scale);
     }
   }
+}
+
+// --------------------------------------------------------------------------
+// bf16 weight gradient on v_mfma_f32_16x16x32_bf16.  K = pixels: both operands
+// are staged pixel-major in LDS ([pixel][o] and the [halo pixel][c] tile) and the
+// k-contiguous fragments are read with ds_read_b64_tr_b16 (gfx950 transposed
+// read: 16 lanes fetch a 4-row x 16-column block, lane i receives column i),
+// whose per-lane row addresses also apply the 3x3 tap shift.  A wave owns
+// MO x NC 16x16 (o, c) blocks for all 9 taps; KW waves split the pixel k-steps
+// and are reduced through LDS; one fp32 atomic per (o, c, tap) per workgroup.
+// --------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
+
+__device__ __forceinline__ bf16x8_t tr_read8(const bf16_t* lo, const bf16_t* hi) {
+  bf16x4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)lo);
+  bf16x4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)hi);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+struct WgBParams {
+  const bf16_t* x;
+  const bf16_t* gz;
+  float* dw;
+  float* db;
+  int B, H, W, Hin, Win;
+  int cin, cout, x_cs, gz_cs;
+  int ups;
+  float scale;
+  int NB, TH, TW, tiles_x, tiles_y, ntiles, tiles_per_split;
+  int GZS, HS, halo_elems;
+};
+
+constexpr int WGB_BP = 128;
+
+template <int MO, int NC, int WMO, int WNC>
+__global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
+  constexpr int KW = 4 / (WMO * WNC);
+  constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* gzl = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* hal = gzl + WGB_BP * p.GZS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid % KW, wmn = wid / KW;
+  const int wo = wmn / WNC, wc = wmn % WNC;
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
+  const int o0 = blockIdx.x * BO, c0 = blockIdx.y * BC;
+  const int TW2 = p.TW + 2, HW2 = (p.TH + 2) * TW2;
+
+  f32x4_t acc[MO][NC][9];
+#pragma unroll
+  for (int a = 0; a < MO; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[a][b][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  float bsum = 0.f;   // bias gradient of output channel o0 + tid (c-tile 0 only)
+  const bool do_db = p.db && blockIdx.y == 0 && tid < BO;
+  const int t_begin = blockIdx.z * p.tiles_per_split;
+  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
+  for (int t = t_begin; t < t_end; ++t) {
+    int tt = t;
+    const int tx0 = (tt % p.tiles_x) * p.TW;
+    tt /= p.tiles_x;
+    const int ty0 = (tt % p.tiles_y) * p.TH;
+    tt /= p.tiles_y;
+    const int b0 = tt * p.NB;
+    __syncthreads();
+    constexpr int GV = BO / 8;
+    for (int i = tid; i < WGB_BP * GV; i += 256) {
+      const int pm = i / GV, v = i - pm * GV;
+      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int b = b0 + nb, o = o0 + 8 * v;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (b < p.B && o < p.cout)
+        val = *reinterpret_cast<const u32x4_t*>(
+            p.gz + (((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx) * p.gz_cs + o);
+      *reinterpret_cast<u32x4_t*>(gzl + pm * p.GZS + 8 * v) = val;
+    }
+    constexpr int HV = BC / 8;
+    for (int i = tid; i < p.halo_elems * HV; i += 256) {
+      const int hp = i / HV, v = i - hp * HV;
+      const int nb = hp / HW2, rem = hp - nb * HW2;
+      const int hy = rem / TW2, hx = rem - hy * TW2;
+      const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1, c = c0 + 8 * v;
+      u32x4_t val = {0u, 0u, 0u, 0u};
+      if (b < p.B && c < p.x_cs && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
+        const int sy = p.ups ? (yy >> 1) : yy, sx = p.ups ? (xx >> 1) : xx;
+        val = *reinterpret_cast<const u32x4_t*>(
+            p.x + (((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + c);
+      }
+      *reinterpret_cast<u32x4_t*>(hal + hp * p.HS + 8 * v) = val;
+    }
+    __syncthreads();
+    if (do_db)
+      for (int pm = 0; pm < WGB_BP; ++pm) bsum += bf2f(gzl[pm * p.GZS + tid]);
+    for (int ks = wk; ks < WGB_BP / 32; ks += KW) {
+      const int rA = ks * 32 + 8 * g + q, rB = rA + 4;   // tile pixels of this lane's rows
+      bf16x8_t A[MO];
+#pragma unroll
+      for (int mo = 0; mo < MO; ++mo) {
+        const int ol = (wo * MO + mo) * 16 + 4 * pq;
+        A[mo] = tr_read8(gzl + rA * p.GZS + ol, gzl + rB * p.GZS + ol);
+      }
+      const int txA = rA % p.TW, tyA = (rA / p.TW) % p.TH, nbA = rA / (p.TW * p.TH);
+      const int txB = rB % p.TW, tyB = (rB / p.TW) % p.TH, nbB = rB / (p.TW * p.TH);
+      const int hA = (nbA * (p.TH + 2) + tyA) * TW2 + txA;
+      const int hB = (nbB * (p.TH + 2) + tyB) * TW2 + txB;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = (tap / 3) * TW2 + (tap % 3);
+#pragma unroll
+        for (int nc = 0; nc < NC; ++nc) {
+          const int cl = (wc * NC + nc) * 16 + 4 * pq;
+          const bf16x8_t Bf = tr_read8(hal + (hA + toff) * p.HS + cl, hal + (hB + toff) * p.HS + cl);
+#pragma unroll
+          for (int mo = 0; mo < MO; ++mo)
+            acc[mo][nc][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mo], Bf, acc[mo][nc][tap],
+                                                                       0, 0, 0);
+        }
+      }
+    }
+  }
+  if (do_db && o0 + tid < p.cout) atomicAdd(p.db + o0 + tid, bsum * p.scale);
+  if (KW > 1) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);   // [KW][wmn][MO][NC][9][64][4]
+    constexpr int PER = MO * NC * 9 * 64 * 4;
+    float* mine = red + ((size_t)wk * (4 / KW) + wmn) * PER;
+    if (wk > 0) {
+#pragma unroll
+      for (int a = 0; a < MO; ++a)
+#pragma unroll
+        for (int b = 0; b < NC; ++b)
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+            *reinterpret_cast<f32x4_t*>(mine + (((a * NC + b) * 9 + t) * 64 + lane) * 4) = acc[a][b][t];
+    }
+    __syncthreads();
+    if (wk != 0) return;
+    for (int k = 1; k < KW; ++k) {
+      const float* other = red + ((size_t)k * (4 / KW) + wmn) * PER;
+#pragma unroll
+      for (int a = 0; a < MO; ++a)
+#pragma unroll
+        for (int b = 0; b < NC; ++b)
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+            acc[a][b][t] += *reinterpret_cast<const f32x4_t*>(other + (((a * NC + b) * 9 + t) * 64 + lane) * 4);
+    }
+  }
+  // acc[mo][nc][tap][j]: o = o0 + (wo*MO+mo)*16 + 4g + j, c = c0 + (wc*NC+nc)*16 + i16
+#pragma unroll
+  for (int mo = 0; mo < MO; ++mo)
+#pragma unroll
+    for (int nc = 0; nc < NC; ++nc) {
+      const int c = c0 + (wc * NC + nc) * 16 + i16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = o0 + (wo * MO + mo) * 16 + 4 * g + j;
+        if (o < p.cout && c < p.cin) {
+          float* dst = p.dw + ((size_t)o * p.cin + c) * 9;
+#pragma unroll
+          for (int tap = 0; tap < 9; ++tap) atomicAdd(dst + tap, acc[mo][nc][tap][j] * p.scale);
+        }
+      }
+    }
+}
+
+template <int MO, int NC, int WMO, int WNC>
+int launch_wgrad_bf16(const pg_conv_desc* d, const void* x, const void* gz, float scale, float* dw,
+                      float* db, hipStream_t st) {
+  constexpr int KW = 4 / (WMO * WNC);
+  constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
+  TileCfg tc = pick_tile(d->H, d->W, WGB_BP, 32);
+  WgBParams p;
+  p.x = (const bf16_t*)x; p.gz = (const bf16_t*)gz; p.dw = dw; p.db = db;
+  p.B = d->B; p.H = d->H; p.W = d->W;
+  p.ups = (d->flags & PG_CONV_UPS_IN) ? 1 : 0;
+  p.Hin = p.ups ? d->H / 2 : d->H;
+  p.Win = p.ups ? d->W / 2 : d->W;
+  p.cin = d->cin; p.cout = d->cout; p.x_cs = d->x_cs; p.gz_cs = d->y_cs;
+  p.scale = scale;
+  p.NB = tc.NB; p.TH = tc.TH; p.TW = tc.TW;
+  p.tiles_x = d->W / tc.TW;
+  p.tiles_y = d->H / tc.TH;
+  p.ntiles = pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y;
+  p.GZS = BO + 8;
+  p.HS = BC + 8;
+  p.halo_elems = tc.NB * (tc.TH + 2) * (tc.TW + 2);
+  const int ot = pg_cdiv(d->cout, BO), ct = pg_cdiv(d->cin, BC);
+  int splits = pg_cdiv(512, ot * ct);
+  if (splits > p.ntiles) splits = p.ntiles;
+  if (splits < 1) splits = 1;
+  p.tiles_per_split = pg_cdiv(p.ntiles, splits);
+  splits = pg_cdiv(p.ntiles, p.tiles_per_split);
+  int lds = (WGB_BP * p.GZS + p.halo_elems * p.HS) * 2;
+  const int red = KW > 1 ? 4 * MO * NC * 9 * 64 * 4 * 4 : 0;
+  if (red > lds) lds = red;
+  PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
+  static bool attr_done = false;
+  if (!attr_done) {
+    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC>), dim3(ot, ct, splits), dim3(256), lds,
+                     st, p);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, float scale,
+                        float* dw, float* db, hipStream_t st) {
+  PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
+               "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
+  const int co = d->cout, ci = d->cin;
+  if (co <= 16 && ci <= 16) return launch_wgrad_bf16<1, 1, 1, 1>(d, x, gz, scale, dw, db, st);
+  if (co <= 16 && ci <= 32) return launch_wgrad_bf16<1, 2, 1, 1>(d, x, gz, scale, dw, db, st);
+  if (co <= 32 && ci <= 16) return launch_wgrad_bf16<2, 1, 1, 1>(d, x, gz, scale, dw, db, st);
+  if (co >= 64 && ci >= 64) return launch_wgrad_bf16<2, 2, 2, 2>(d, x, gz, scale, dw, db, st);
+  return launch_wgrad_bf16<1, 1, 2, 2>(d, x, gz, scale, dw, db, st);
 }
 
 // --------------------------------------------------------------------------
@@ -401,23 +647,6 @@ __global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scal
       atomicAdd(db + c, s * scale);
     }
   }
-}
-
-int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
-
-struct TileCfg {
-  int BM, BN, NB, TH, TW;
-};
-
-TileCfg pick_tile(int H, int W, int BM, int BN) {
-  TileCfg t;
-  t.BM = BM;
-  t.BN = BN;
-  t.TW = W < 16 ? W : 16;
-  t.TH = BM / t.TW;
-  if (t.TH > H) t.TH = H;
-  t.NB = BM / (t.TH * t.TW);
-  return t;
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -528,12 +757,13 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
 }
 
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, void* stream) {
+                     float* dw, float* db, void* stream) {
   PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
+  if (dtype == PG_BF16) return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (hipStream_t)stream);
   TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
   WgParams p;
-  p.x = x; p.gz = gz; p.dw = dw;
+  p.x = x; p.gz = gz; p.dw = dw; p.db = db;
   p.B = d->B; p.H = d->H; p.W = d->W;
   p.ups = (d->flags & PG_CONV_UPS_IN) ? 1 : 0;
   p.Hin = p.ups ? d->H / 2 : d->H;

@@ -299,9 +299,10 @@ class StepEngine:
                          flags=flags, slope=SLOPE, out_scale=out_scale,
                          bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2)
 
-    def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False):
+    def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None):
         c = self.packs[(net, key)][3]
-        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c)
+        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c,
+                            db=db)
 
     # ================================================================== G
     def g_forward(self, P, z, alpha):
@@ -358,21 +359,21 @@ class StepEngine:
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
             ops.pixnorm_lrelu_bwd(g[f"ub{i}"], g[f"gy{i + 1}"], g[f"gzb{i}"], d[i + 1], SLOPE)
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
-                        d[i + 1])
-            ops.bias_grad(g[f"gzb{i}"], GR[b + "bias"], d[i + 1], self.packs[("G", f"b{i}")][3])
+                        d[i + 1],
+                        db=GR[b + "bias"])
             self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gya{i}"], Ri, d[i + 1], d[i + 1], 0,
                        dgrad=True)
             ops.pixnorm_lrelu_bwd(g[f"ua{i}"], g[f"gya{i}"], g[f"gza{i}"], d[i + 1], SLOPE)
             self._wgrad("G", f"a{i}", self._ylvl(i), g[f"gza{i}"], GR[a + "weight"], Ri, d[i],
-                        d[i + 1], ups=True)
-            ops.bias_grad(g[f"gza{i}"], GR[a + "bias"], d[i + 1], self.packs[("G", f"a{i}")][3])
+                        d[i + 1], ups=True,
+                        db=GR[a + "bias"])
             flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and s >= 1) else 0)
             self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
                        dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
         fb = "first_block.block.0.module."
         ops.pixnorm_lrelu_bwd(g["u0"], g["gy0"], g["gz0"], d[0], SLOPE)
-        self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0])
-        ops.bias_grad(g["gz0"], GR[fb + "bias"], d[0], self.packs[("G", "first")][3])
+        self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
+                    db=GR[fb + "bias"])
         self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)
         ops.pixnorm_lrelu_bwd(g["f"], g["gh0"], g["gzf"], d[0], self.hyper.slope_cfg)
         ops.linear_wgrad(g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
@@ -428,8 +429,8 @@ class StepEngine:
                          aux=D["c"])
         if GR is not None:
             cv = "minibatch_normalization_block.conv.module."
-            self._wgrad("D", "mb", D["m"], D["gzc"], GR[cv + "weight"], 4, d[0] + 1, d[0])
-            ops.bias_grad(D["gzc"], GR[cv + "bias"], d[0], self.packs[("D", "mb")][3])
+            self._wgrad("D", "mb", D["m"], D["gzc"], GR[cv + "weight"], 4, d[0] + 1, d[0],
+                        db=GR[cv + "bias"])
         self._conv("D", "mb", D["gzc"], D["gm"], 4, d[0], r4(d[0] + 1), 0, dgrad=True)
         ops.mbstd_bwd(self.h_mb, D["gm"], D["gh"], B=B, HW=16, C=d[0])
         if inj_mbstd is not None:
@@ -447,15 +448,15 @@ class StepEngine:
                             slope=SLOPE, ups=True)
             if GR is not None:
                 self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
-                            d[i])
-                ops.bias_grad(D[f"gzb{i}"], GR[b + "bias"], d[i], self.packs[("D", f"b{i}")][3])
+                            d[i],
+                            db=GR[b + "bias"])
             self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_MASK,
                        aux=D[f"a{i}"], dgrad=True)
             hin = D["yrgb"] if i == s - 1 else (D["hblend"] if i == s - 2 else D[f"p{i + 1}"])
             if GR is not None:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
-                            d[i + 1])
-                ops.bias_grad(D[f"gza{i}"], GR[a + "bias"], d[i + 1], self.packs[("D", f"a{i}")][3])
+                            d[i + 1],
+                            db=GR[a + "bias"])
             if i == s - 1:
                 self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
                            L.CONV_MASK, aux=D["yrgb"], dgrad=True)

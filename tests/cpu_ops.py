@@ -99,12 +99,14 @@ class CpuOps:
         else:
             y[..., :cout] = z
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale):
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None):
         xin = nchw(x, cin)
         if ups:
             xin = up2(xin)
         g = nchw(gz, cout)
         dw += scale * torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), g, padding=1)
+        if db is not None:
+            db += scale * g.sum((0, 2, 3))
 
     def bias_grad(self, g, db, C, scale):
         db += scale * g[..., :C].reshape(-1, C).sum(0)
