@@ -51,6 +51,7 @@ class KernelTimer:
 
     def __init__(self, ops):
         self.rec = {"conv3x3": [], "wgrad3x3": []}
+        self.shapes = []
         self.on = False
         f_conv, f_wg = ops.conv3x3, ops.conv_wgrad
 
@@ -63,6 +64,7 @@ class KernelTimer:
             b.record()
             fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
             self.rec["conv3x3"].append((a, b, fl))
+            self.shapes.append(("conv3x3", kw["H"], kw["cin"], kw["cout"], kw["flags"], a, b, fl))
 
         def conv_wgrad(x, gz, dw, **kw):
             if not self.on:
@@ -73,8 +75,23 @@ class KernelTimer:
             b.record()
             fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
             self.rec["wgrad3x3"].append((a, b, fl))
+            self.shapes.append(("wgrad3x3", kw["H"], kw["cin"], kw["cout"], int(kw["ups"]), a, b,
+                                fl))
 
         ops.conv3x3, ops.conv_wgrad = conv3x3, conv_wgrad
+
+    def per_shape(self, steps):
+        agg = {}
+        for k, H, ci, co, fl, a, b, f in self.shapes:
+            key = (k, H, ci, co, fl)
+            t = agg.setdefault(key, [0.0, 0.0, 0])
+            t[0] += a.elapsed_time(b)
+            t[1] += f
+            t[2] += 1
+        rows = sorted(agg.items(), key=lambda kv: -kv[1][0])
+        return [dict(kernel=k[0], H=k[1], cin=k[2], cout=k[3], flags=k[4],
+                     ms_per_step=round(v[0] / steps, 3), tflops=round(v[1] / (v[0] * 1e-3) / 1e12, 1),
+                     calls_per_step=v[2] // steps) for k, v in rows]
 
     def summary(self):
         out = {}
@@ -191,6 +208,9 @@ def main():
     dt = float(t.item())
     assert torch.isfinite(eng.loss).all(), "non-finite loss"
     ksum = timer.summary() if timer else {}
+    if timer and os.environ.get("PG_BENCH_SHAPES"):
+        with open(os.environ["PG_BENCH_SHAPES"], "w") as f:
+            json.dump(timer.per_shape(args.steps), f, indent=1)
 
     if rank == 0:
         roof = None

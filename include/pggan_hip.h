@@ -66,8 +66,13 @@ typedef struct {
 size_t pg_conv3x3_packed_elems(int mode, int cout, int cin);
 int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw, float scale,
                     void* wpk, void* stream);
+/* ws: optional fp32 workspace (>= pg_conv3x3_workspace_size bytes) that enables split-K
+ * over input-channel chunks for small-spatial convs (deterministic: partial slabs + a
+ * reduction/epilogue kernel); NULL or too small -> single pass. */
+size_t pg_conv3x3_workspace_size(const pg_conv_desc* d);
 int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
-                   const float* bias, const void* aux, void* y, void* y2, void* stream);
+                   const float* bias, const void* aux, void* y, void* y2, void* ws,
+                   size_t ws_bytes, void* stream);
 /* weight gradient, accumulates: dw[o][c][ky][kx] += scale * sum_p gz[p][o] * x[p+tap][c]
  * and, if db != NULL, the bias gradient db[o] += scale * sum_p gz[p][o] (fused: gz is read
  * once).  desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold

@@ -42,7 +42,9 @@ _SIGS = {
     "pg_version": ([], _I),
     "pg_conv3x3_packed_elems": ([_I, _I, _I], _SZ),
     "pg_conv3x3_pack": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
-    "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_conv3x3_workspace_size": ([ctypes.POINTER(ConvDesc)], _SZ),
+    "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
+                       _I),
     "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP], _I),
     "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
@@ -136,13 +138,20 @@ class HipOps:
                                            self._s()), "conv3x3_pack")
 
     def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
-                bias=None, aux=None, y2=None):
-        self._cuda(x, wpk, y, bias, aux, y2)
+                bias=None, aux=None, y2=None, ws=None):
+        """ws: optional fp32 workspace tensor enabling split-K (see conv_workspace_bytes)."""
+        self._cuda(x, wpk, y, bias, aux, y2, ws)
         d = ConvDesc(B, H, W, cin, cout, x.shape[-1], y.shape[-1],
                      aux.shape[-1] if aux is not None else 0,
                      y2.shape[-1] if y2 is not None else 0, flags, slope, out_scale)
+        wsb = ws.numel() * ws.element_size() if ws is not None else 0
         self._chk(self.lib.pg_conv3x3_fwd(self._dt(y), ctypes.byref(d), _p(x), _p(wpk), _p(bias),
-                                          _p(aux), _p(y), _p(y2), self._s()), "conv3x3_fwd")
+                                          _p(aux), _p(y), _p(y2), _p(ws), wsb, self._s()),
+                  "conv3x3_fwd")
+
+    def conv_workspace_bytes(self, *, B, H, W, cin, cout):
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, 0, 0.0, 1.0)
+        return int(self.lib.pg_conv3x3_workspace_size(ctypes.byref(d)))
 
     def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None):
         self._cuda(x, gz, dw, db)

@@ -37,6 +37,10 @@ struct ConvParams {
   int NB, TH, TW, tiles_x, tiles_y;
   int CK, KS, nchunks;
   int pixb, wrowb, halo_bytes;
+  // split-K: blockIdx.z sums chunks [z*cps, (z+1)*cps) into fp32 slab z of ws
+  float* ws;
+  int cps;
+  size_t slab;   // elements per slab = B*H*W*cout_p
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
@@ -127,7 +131,9 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const int vpp = p.CK * (int)sizeof(T) / 16;  // 16-byte vectors per halo pixel / per tap
   const int ntap_pad = p.KS * 32 / p.CK;
 
-  for (int ch = 0; ch < p.nchunks; ++ch) {
+  const int ch_begin = blockIdx.z * p.cps;
+  const int ch_end = min(p.nchunks, ch_begin + p.cps);
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
     const int c0 = ch * p.CK;
     __syncthreads();
     for (int i = tid; i < npix_halo * vpp; i += 256) {
@@ -179,8 +185,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   __syncthreads();
   float* ot = reinterpret_cast<float*>(smem);
   constexpr int ORS = BN + 4;
-  const bool has_bias = (p.flags & PG_CONV_BIAS) != 0;
-  const bool do_lrelu = (p.flags & PG_CONV_LRELU) != 0;
+  const bool has_bias = !p.ws && (p.flags & PG_CONV_BIAS) != 0;   // split-K: raw sums
+  const bool do_lrelu = !p.ws && (p.flags & PG_CONV_LRELU) != 0;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int nl = wn * (BN / WN) + nt * 16 + r;
@@ -203,7 +209,20 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const bool do_mask = (p.flags & PG_CONV_MASK) != 0;
   const bool do_acc = (p.flags & PG_CONV_ACCUM) != 0;
   T* y = reinterpret_cast<T*>(p.y);
-  if (!(p.flags & PG_CONV_POOL)) {
+  if (p.ws) {   // split-K partial: raw fp32 sums to this split's slab, [pixel][cout_p]
+    float* slab = p.ws + blockIdx.z * p.slab;
+    for (int i = tid; i < BM * NV; i += 256) {
+      const int pm = i / NV, cv = (i - pm * NV) * 4;
+      const int n = n0 + cv;
+      if (n >= p.cout_p) continue;
+      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int b = b0 + nb;
+      if (b >= p.B) continue;
+      const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
+      *reinterpret_cast<f32x4_t*>(slab + pix * p.cout_p + n) =
+          *reinterpret_cast<const f32x4_t*>(ot + pm * ORS + cv);
+    }
+  } else if (!(p.flags & PG_CONV_POOL)) {
     for (int i = tid; i < BM * NV; i += 256) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
@@ -271,6 +290,60 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       }
       Ty<T>::st4(dst, v);
     }
+  }
+}
+
+// Split-K reduction + epilogue: y = out_scale * post(sum_z slab_z + bias) with the same
+// flag semantics as conv3x3_kernel's epilogue (bias, lrelu, 2x2 pool (+ y2), mask, accum).
+template <typename T>
+__global__ void conv_splitk_epilogue(ConvParams p, int splits) {
+  const int nv = p.cout >> 2;
+  const bool pool = (p.flags & PG_CONV_POOL) != 0;
+  const int Ho = pool ? p.H >> 1 : p.H, Wo = pool ? p.W >> 1 : p.W;
+  const size_t n = (size_t)p.B * Ho * Wo * nv;
+  T* y = reinterpret_cast<T*>(p.y);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % nv) * 4;
+    const size_t op = i / nv;
+    const int xo = (int)(op % Wo), yo = (int)((op / Wo) % Ho), b = (int)(op / ((size_t)Wo * Ho));
+    float bsv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bsv[q] = (p.flags & PG_CONV_BIAS) ? p.bias[c + q] : 0.f;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int np = pool ? 4 : 1;
+    for (int k = 0; k < np; ++k) {
+      const int yy = pool ? 2 * yo + (k >> 1) : yo, xx = pool ? 2 * xo + (k & 1) : xo;
+      const size_t pix = ((size_t)b * p.H + yy) * p.W + xx;
+      float a[4] = {bsv[0], bsv[1], bsv[2], bsv[3]};
+      for (int z = 0; z < splits; ++z) {
+        const f32x4_t t = *reinterpret_cast<const f32x4_t*>(p.ws + z * p.slab + pix * p.cout_p + c);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] += t[q];
+      }
+      if (p.flags & PG_CONV_LRELU)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = lrelu_f(a[q], p.slope);
+      if (pool && p.y2) Ty<T>::st4(reinterpret_cast<T*>(p.y2) + pix * p.y2_cs + c, a);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += a[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] *= p.out_scale;
+    if (p.flags & PG_CONV_MASK) {
+      float m[4];
+      Ty<T>::ld4(reinterpret_cast<const T*>(p.aux) + op * p.aux_cs + c, m);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= lmask_f(m[q], p.slope);
+    }
+    T* dst = y + op * p.y_cs + c;
+    if (p.flags & PG_CONV_ACCUM) {
+      float o[4];
+      Ty<T>::ld4(dst, o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] += o[q];
+    }
+    Ty<T>::st4(dst, v);
   }
 }
 
@@ -527,22 +600,37 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
             acc[a][b][t] += *reinterpret_cast<const f32x4_t*>(other + (((a * NC + b) * 9 + t) * 64 + lane) * 4);
     }
   }
-  // acc[mo][nc][tap][j]: o = o0 + (wo*MO+mo)*16 + 4g + j, c = c0 + (wc*NC+nc)*16 + i16
+  // acc[mo][nc][tap][j]: o = o0 + (wo*MO+mo)*16 + 4g + j, c = c0 + (wc*NC+nc)*16 + i16.
+  // Transpose each (mo, nc, j) slice through a per-wave LDS scratch so that every atomic
+  // wave-instruction covers contiguous [c][tap] runs of one OIHW row (full atomic rate;
+  // lanes 36 B apart would hit ~36 lines per instruction).
+  if (KW == 1) __syncthreads();
+  float* scr = reinterpret_cast<float*>(smem) +
+               (KW > 1 ? (size_t)wmn * (MO * NC * 9 * 64 * 4) : (size_t)wid * 576);
 #pragma unroll
   for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
-    for (int nc = 0; nc < NC; ++nc) {
-      const int c = c0 + (wc * NC + nc) * 16 + i16;
+    for (int nc = 0; nc < NC; ++nc)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int o = o0 + (wo * MO + mo) * 16 + 4 * g + j;
-        if (o < p.cout && c < p.cin) {
-          float* dst = p.dw + ((size_t)o * p.cin + c) * 9;
 #pragma unroll
-          for (int tap = 0; tap < 9; ++tap) atomicAdd(dst + tap, acc[mo][nc][tap][j] * p.scale);
+        for (int tap = 0; tap < 9; ++tap) scr[(g * 16 + i16) * 9 + tap] = acc[mo][nc][tap][j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int it = 0; it < 9; ++it) {
+          const int idx = it * 64 + lane;
+          const int gg = idx / 144, rem = idx - gg * 144;
+          const int c = c0 + (wc * NC + nc) * 16 + rem / 9, tap = rem % 9;
+          const int o = o0 + (wo * MO + mo) * 16 + 4 * gg + j;
+          if (o < p.cout && c < p.cin)
+            atomicAdd(p.dw + ((size_t)o * p.cin + c) * 9 + tap, scr[idx] * p.scale);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
-    }
 }
 
 template <int MO, int NC, int WMO, int WNC>
@@ -567,8 +655,10 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const void* x, const void* gz, floa
   p.HS = BC + 8;
   p.halo_elems = tc.NB * (tc.TH + 2) * (tc.TW + 2);
   const int ot = pg_cdiv(d->cout, BO), ct = pg_cdiv(d->cin, BC);
+  // >= 4 pixel tiles per workgroup keeps the atomic bytes per MFMA flop low
   int splits = pg_cdiv(512, ot * ct);
-  if (splits > p.ntiles) splits = p.ntiles;
+  const int max_splits = p.ntiles / 4 > 1 ? p.ntiles / 4 : 1;
+  if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   p.tiles_per_split = pg_cdiv(p.ntiles, splits);
   splits = pg_cdiv(p.ntiles, p.tiles_per_split);
@@ -649,9 +739,39 @@ __global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scal
   }
 }
 
+void conv_tile_for(int cout, int* BM, int* BN) {
+  const int cout_p = (cout + 15) & ~15;
+  if (cout_p >= 64) { *BM = 128; *BN = 64; }
+  else if (cout_p >= 32) { *BM = 256; *BN = 32; }
+  else { *BM = 256; *BN = 16; }
+}
+
+// split-K factor: spread the channel chunks of small-spatial / wide convs (4x4..16x16 at
+// 512 channels launch only 8..64 output tiles) over enough workgroups to fill the chip
+int conv_splits(const pg_conv_desc* d) {
+  int BM, BN;
+  conv_tile_for(d->cout, &BM, &BN);
+  TileCfg tc = pick_tile(d->H, d->W, BM, BN);
+  const int cout_p = (d->cout + 15) & ~15;
+  const int base = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH) * pg_cdiv(cout_p, BN);
+  const int cin_p = cinp_of(d->cin);
+  const int nch = cin_p / (cin_p < 32 ? cin_p : 32);
+  if (base >= 128 || nch < 4) return 1;
+  int sp = pg_cdiv(256, base);
+  if (sp > nch) sp = nch;
+  const int cps = pg_cdiv(nch, sp);
+  return pg_cdiv(nch, cps);
+}
+
+size_t conv_ws_bytes(const pg_conv_desc* d) {
+  const int sp = conv_splits(d);
+  if (sp <= 1) return 0;
+  return (size_t)sp * d->B * d->H * d->W * ((d->cout + 15) & ~15) * sizeof(float);
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
-                const void* aux, void* y, void* y2, hipStream_t st) {
+                const void* aux, void* y, void* y2, void* ws, size_t ws_bytes, hipStream_t st) {
   TileCfg tc = pick_tile(d->H, d->W, BM, BN);
   ConvParams p;
   p.x = x; p.w = wpk; p.bias = bias; p.aux = aux; p.y = y; p.y2 = y2;
@@ -678,7 +798,14 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   const int epi_bytes = BM * (BN + 4) * 4;
   const int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   PG_CHECK_ARG(lds <= 160 * 1024, "conv3x3: LDS %d bytes too large", lds);
-  dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0));
+  int splits = 1;
+  const size_t need = conv_ws_bytes(d);
+  if (need && ws && ws_bytes >= need) splits = conv_splits(d);
+  p.ws = splits > 1 ? (float*)ws : nullptr;
+  p.cps = pg_cdiv(p.nchunks, splits);
+  p.slab = (size_t)d->B * d->H * d->W * p.cout_p;
+  dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
+            splits);
   static bool attr_done = false;
   if (!attr_done) {
     (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN>,
@@ -686,17 +813,25 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
     attr_done = true;
   }
   hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN>), grid, dim3(256), lds, st, p);
+  if (splits > 1) {
+    const bool pool = (d->flags & PG_CONV_POOL) != 0;
+    const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(conv_splitk_epilogue<T>, dim3(blocks), dim3(256), 0, st, p, splits);
+  }
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
 
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
-                  const void* aux, void* y, void* y2, hipStream_t st) {
-  const int cout_p = (d->cout + 15) & ~15;
-  if (cout_p >= 64) return launch_conv<T, 128, 64, 2, 2>(d, x, wpk, bias, aux, y, y2, st);
-  if (cout_p >= 32) return launch_conv<T, 256, 32, 4, 1>(d, x, wpk, bias, aux, y, y2, st);
-  return launch_conv<T, 256, 16, 4, 1>(d, x, wpk, bias, aux, y, y2, st);
+                  const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
+  int BM, BN;
+  conv_tile_for(d->cout, &BM, &BN);
+  if (BN == 64) return launch_conv<T, 128, 64, 2, 2>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  if (BN == 32) return launch_conv<T, 256, 32, 4, 1>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  return launch_conv<T, 256, 16, 4, 1>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
 }
 
 }  // namespace
@@ -732,8 +867,11 @@ int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw,
   return PG_OK;
 }
 
+size_t pg_conv3x3_workspace_size(const pg_conv_desc* d) { return d ? conv_ws_bytes(d) : 0; }
+
 int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
-                   const float* bias, const void* aux, void* y, void* y2, void* stream) {
+                   const float* bias, const void* aux, void* y, void* y2, void* ws,
+                   size_t ws_bytes, void* stream) {
   PG_CHECK_ARG(d && x && wpk && y, "conv3x3_fwd: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4 && (d->H & (d->H - 1)) == 0 &&
                    (d->W & (d->W - 1)) == 0,
@@ -752,8 +890,8 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
   PG_CHECK_ARG(!y2 || (d->flags & PG_CONV_POOL), "conv3x3_fwd: y2 only with POOL");
   PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, st);
-  return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, st);
+  if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
+  return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
 }
 
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,

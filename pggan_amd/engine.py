@@ -166,6 +166,7 @@ class StepEngine:
         self.d0 = d[0]
         self.mcs = cinp(d[0] + 1)
         self.keep_fake_D = False
+        self.ws = None          # split-K workspace (fp32), grown on first use
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -295,9 +296,13 @@ class StepEngine:
         pf, pd, bs, _ = self.packs[(net, key)]
         if not dgrad and bias:
             flags |= L.CONV_BIAS
+        need = self.ops.conv_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout)
+        if need and (self.ws is None or self.ws.numel() * 4 < need):
+            self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         self.ops.conv3x3(x, pd if dgrad else pf, y, B=self.B, H=H, W=H, cin=cin, cout=cout,
                          flags=flags, slope=SLOPE, out_scale=out_scale,
-                         bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2)
+                         bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2,
+                         ws=self.ws if need else None)
 
     def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None):
         c = self.packs[(net, key)][3]

@@ -74,8 +74,11 @@ class CpuOps:
             P[:cin, :, :cout] = scale * w9.flip(2).permute(1, 2, 0)
         out.copy_(P.reshape(-1))
 
+    def conv_workspace_bytes(self, *, B, H, W, cin, cout):
+        return 0
+
     def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
-                bias=None, aux=None, y2=None):
+                bias=None, aux=None, y2=None, ws=None):
         ci, co = cinp(cin), r16(cout)
         Wt = wpk.view(co, 9, ci).permute(0, 2, 1).reshape(co, ci, 3, 3)[:cout]
         xin = nchw(x, ci)

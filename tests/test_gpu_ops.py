@@ -322,3 +322,47 @@ def test_randn_moments():
     z2 = torch.empty(1 << 20, device="cuda")
     hip.randn(z2, 1234, 0)
     assert torch.equal(z, z2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", [(4, 8, 512, 512, ("bias", "lrelu")),
+                                  (4, 16, 512, 512, ("bias", "lrelu", "pool")),
+                                  (4, 4, 513, 512, ("bias", "lrelu")),
+                                  (4, 4, 512, 516, ()),
+                                  (4, 8, 512, 512, ("mask", "accum")),
+                                  (3, 8, 256, 64, ("ups", "bias", "lrelu"))])
+def test_conv3x3_splitk(case, dtype):
+    """Small-spatial wide convs take the split-K path (fp32 partial slabs + epilogue)."""
+    B, H, cin, cout, fl = case
+    _L = lib()
+    hip, cpu = ops_pair(dtype)
+    flags = 0
+    for f, v in (("ups", _L.CONV_UPS_IN), ("bias", _L.CONV_BIAS), ("lrelu", _L.CONV_LRELU),
+                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM)):
+        if f in fl:
+            flags |= v
+    need = hip.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
+    assert need > 0, "expected the split-K path for this shape"
+    Hin = H // 2 if "ups" in fl else H
+    x = q(rnd(B, Hin, Hin, cinp(cin), seed=81), dtype)
+    x[..., cin:] = 0
+    w = rnd(cout, cin, 3, 3, seed=82)
+    bias = rnd(cout, seed=83) * 0.1
+    Ho = H // 2 if "pool" in fl else H
+    y0 = q(rnd(B, Ho, Ho, cout, seed=84), dtype)
+    aux = q(rnd(B, H, H, cout, seed=85), dtype)
+    outs = []
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        wp = torch.zeros(ops.packed_elems(0, cout, cin), dtype=dt, device=dev)
+        ops.conv_pack(0, w.to(dev), 0.02, wp)
+        y = y0.to(dev).to(dt).clone()
+        y2 = torch.zeros(B, H, H, cout, dtype=dt, device=dev) if "pool" in fl else None
+        ws = torch.empty(need // 4, device=dev) if dev == "cuda" else None
+        ops.conv3x3(x.to(dev).to(dt), wp, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
+                    out_scale=0.25 if "pool" in fl else 1.0, bias=(bias * 0.02).to(dev),
+                    aux=aux.to(dev).to(dt), y2=y2, ws=ws)
+        outs.append((y, y2))
+    cmp(outs[0][0], outs[1][0], tol_for(dtype), "splitk y")
+    if outs[0][1] is not None:
+        cmp(outs[0][1], outs[1][1], tol_for(dtype), "splitk y2")

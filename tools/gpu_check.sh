@@ -29,6 +29,7 @@ for step in "$@"; do
           --cpu-baseline off --no-kernel-events ) > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -n 3 gpurun_out/prof.log
       if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    shapes) PG_BENCH_SHAPES=gpurun_out/shapes.json run shapes 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
