@@ -22,6 +22,8 @@
 
 namespace {
 
+constexpr int CONV_MAXV = 16;   // max staged 16-byte vectors per thread per chunk
+
 struct ConvParams {
   const void* x;
   const void* w;
@@ -130,37 +132,65 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const bool ups = (p.flags & PG_CONV_UPS_IN) != 0;
   const int vpp = p.CK * (int)sizeof(T) / 16;  // 16-byte vectors per halo pixel / per tap
   const int ntap_pad = p.KS * 32 / p.CK;
+  constexpr int EPV = 16 / (int)sizeof(T);     // elements per 16-byte vector
 
-  const int ch_begin = blockIdx.z * p.cps;
-  const int ch_end = min(p.nchunks, ch_begin + p.cps);
-  for (int ch = ch_begin; ch < ch_end; ++ch) {
-    const int c0 = ch * p.CK;
-    __syncthreads();
-    for (int i = tid; i < npix_halo * vpp; i += 256) {
+  // Staging plan, computed once: this thread's 16-byte vectors of the halo tile and of
+  // the weight slab (element offset in x / w without the chunk's channel base, -1 = zero
+  // fill) and their LDS byte offsets.  Each chunk is then fetched into registers one
+  // chunk ahead (issued before the MFMAs of the current chunk, written to LDS after).
+  int soff[CONV_MAXV], loff[CONV_MAXV];
+  unsigned wmask = 0;
+  const int nhv = npix_halo * vpp;
+  const int ntot = nhv + BN * ntap_pad * vpp;
+#pragma unroll
+  for (int j = 0; j < CONV_MAXV; ++j) {
+    const int i = tid + 256 * j;
+    soff[j] = -1;
+    loff[j] = -1;
+    if (i < nhv) {
       const int hp = i / vpp, v = i - hp * vpp;
       const int nb = hp / HW2, rem = hp - nb * HW2;
       const int hy = rem / TW2, hx = rem - hy * TW2;
       const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1;
-      u32x4_t val = {0u, 0u, 0u, 0u};
+      loff[j] = hp * p.pixb + v * 16;
       if (b < p.B && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
         const int sy = ups ? (yy >> 1) : yy, sx = ups ? (xx >> 1) : xx;
-        const char* src = (const char*)p.x +
-                          ((((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + c0) * sizeof(T) + v * 16;
-        val = *reinterpret_cast<const u32x4_t*>(src);
+        soff[j] = (int)((((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + v * EPV);
       }
-      *reinterpret_cast<u32x4_t*>(halo + hp * p.pixb + v * 16) = val;
-    }
-    for (int i = tid; i < BN * ntap_pad * vpp; i += 256) {
-      const int row = i / (ntap_pad * vpp), rem = i - row * (ntap_pad * vpp);
+    } else if (i < ntot) {
+      const int iw = i - nhv;
+      const int row = iw / (ntap_pad * vpp), rem = iw - row * (ntap_pad * vpp);
       const int tap = rem / vpp, v = rem - tap * vpp;
       const int n = n0 + row;
-      u32x4_t val = {0u, 0u, 0u, 0u};
-      if (tap < 9 && n < p.cout_p)
-        val = *reinterpret_cast<const u32x4_t*>(
-            (const char*)p.w + (((size_t)n * 9 + tap) * p.cin_p + c0) * sizeof(T) + v * 16);
-      *reinterpret_cast<u32x4_t*>(wl + row * p.wrowb + tap * p.CK * sizeof(T) + v * 16) = val;
+      loff[j] = p.halo_bytes + row * p.wrowb + tap * p.CK * (int)sizeof(T) + v * 16;
+      wmask |= 1u << j;
+      if (tap < 9 && n < p.cout_p) soff[j] = (n * 9 + tap) * p.cin_p + v * EPV;
     }
+  }
+  const T* xs = reinterpret_cast<const T*>(p.x);
+  const T* wsrc = reinterpret_cast<const T*>(p.w);
+  u32x4_t buf[CONV_MAXV];
+  auto prefetch = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < CONV_MAXV; ++j) {
+      buf[j] = u32x4_t{0u, 0u, 0u, 0u};
+      if (soff[j] >= 0) {
+        const T* base = ((wmask >> j) & 1u) ? wsrc : xs;
+        buf[j] = *reinterpret_cast<const u32x4_t*>(base + soff[j] + c0);
+      }
+    }
+  };
+
+  const int ch_begin = blockIdx.z * p.cps;
+  const int ch_end = min(p.nchunks, ch_begin + p.cps);
+  if (ch_begin < ch_end) prefetch(ch_begin * p.CK);
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
     __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CONV_MAXV; ++j)
+      if (loff[j] >= 0) *reinterpret_cast<u32x4_t*>(smem + loff[j]) = buf[j];
+    __syncthreads();
+    if (ch + 1 < ch_end) prefetch((ch + 1) * p.CK);
     for (int ks = 0; ks < p.KS; ++ks) {
       const int k0 = ks * 32 + 8 * g;
       int tap = k0 / p.CK;
@@ -787,7 +817,9 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.NB = tc.NB; p.TH = tc.TH; p.TW = tc.TW;
   p.tiles_x = d->W / tc.TW;
   p.tiles_y = d->H / tc.TH;
-  p.CK = p.cin_p < 32 ? p.cin_p : 32;
+  // channels per chunk: 32 (bf16) / 16 (f32) keeps the staged chunk at 64 B per halo pixel
+  const int ck_max = sizeof(T) == 4 ? 16 : 32;
+  p.CK = p.cin_p < ck_max ? p.cin_p : ck_max;
   p.KS = (9 * p.CK + 31) / 32;
   p.nchunks = p.cin_p / p.CK;
   const int pb = p.CK * (int)sizeof(T);
@@ -798,6 +830,12 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   const int epi_bytes = BM * (BN + 4) * 4;
   const int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   PG_CHECK_ARG(lds <= 160 * 1024, "conv3x3: LDS %d bytes too large", lds);
+  {
+    const int vpp = p.CK * (int)sizeof(T) / 16;
+    const int ntot = tc.NB * (tc.TH + 2) * (tc.TW + 2) * vpp + BN * (p.KS * 32 / p.CK) * vpp;
+    PG_CHECK_ARG(ntot <= 256 * CONV_MAXV, "conv3x3: %d staged vectors exceed %d per block", ntot,
+                 256 * CONV_MAXV);
+  }
   int splits = 1;
   const size_t need = conv_ws_bytes(d);
   if (need && ws && ws_bytes >= need) splits = conv_splits(d);

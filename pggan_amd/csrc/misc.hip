@@ -308,6 +308,68 @@ __global__ void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x, flo
   }
 }
 
+// Register-accumulating wgrad of the 1x1 RGB layers for small channel counts (the
+// 512^2 / 1024^2 layers with 16-32 channels are where these bytes are): one pixel per
+// thread per iteration, NA accumulators per thread, butterfly + LDS block reduction,
+// one atomic per accumulator per block.
+// accumulators [0, NW) go to dw[q], [NW, NA) to db[q - NW] (either may be NULL)
+template <int NA, int NW>
+__device__ __forceinline__ void block_reduce_atomic(float (&a)[NA], float* red, float* dw,
+                                                    float* db, float scale) {
+#pragma unroll
+  for (int q = 0; q < NA; ++q) a[q] = wave_sum(a[q]);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NA; ++q) red[wid * NA + q] = a[q];
+  __syncthreads();
+  for (int q = threadIdx.x; q < NA; q += blockDim.x) {
+    float t = 0.f;
+    for (int w = 0; w < nw; ++w) t += red[w * NA + q];
+    float* d = q < NW ? (dw ? dw + q : nullptr) : (db ? db + (q - NW) : nullptr);
+    if (d) atomicAdd(d, t * scale);
+  }
+}
+
+// toRGB wgrad: dw[o][k] += f * sum_pix g[o][pix] x[pix][k], db[o] += f * sum g[o][pix]
+template <typename T, int C>
+__global__ __launch_bounds__(256) void rgb_wgrad_small(int B, int Rx, int x_cs, const T* x, float f, int child,
+                                const float* gimg, float* dw, float* db) {
+  __shared__ float red[4 * (3 * C + 3)];
+  const int Ri = child ? 2 * Rx : Rx;
+  const size_t npix = (size_t)B * Rx * Rx;
+  float acc[3 * C + 3];
+#pragma unroll
+  for (int q = 0; q < 3 * C + 3; ++q) acc[q] = 0.f;
+  for (size_t pp = blockIdx.x * (size_t)blockDim.x + threadIdx.x; pp < npix;
+       pp += (size_t)gridDim.x * blockDim.x) {
+    const int px = (int)(pp % Rx), py = (int)((pp / Rx) % Rx), bi = (int)(pp / ((size_t)Rx * Rx));
+    float gv[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float* gp = gimg + ((size_t)bi * 3 + o) * Ri * Ri;
+      if (!child) {
+        gv[o] = gp[(size_t)py * Ri + px];
+      } else {
+        const size_t a = (size_t)(2 * py) * Ri + 2 * px;
+        gv[o] = gp[a] + gp[a + 1] + gp[a + Ri] + gp[a + Ri + 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < C; k += 4) {
+      float v[4];
+      Ty<T>::ld4(x + pp * x_cs + k, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int o = 0; o < 3; ++o) acc[o * C + k + j] += gv[o] * v[j];
+    }
+#pragma unroll
+    for (int o = 0; o < 3; ++o) acc[3 * C + o] += gv[o];
+  }
+  block_reduce_atomic<3 * C + 3, 3 * C>(acc, red, dw, db, f);
+}
+
 __device__ __forceinline__ void img_in3(const float* img, int bi, int R, int py, int px, int down,
                                         float v[3]) {
   if (!down) {
@@ -438,6 +500,36 @@ __global__ void from_rgb_wgrad_kernel(int B, int R, int C, const float* img, int
   }
 }
 
+// fromRGB wgrad for small C: dw[o][i] += c sum gz[pix][o] img_in[i][pix], db[o] += c sum gz
+template <typename T, int C>
+__global__ __launch_bounds__(256) void from_rgb_wgrad_small(int B, int R, const float* img, int down, float c,
+                                     int gz_cs, const T* gz, float* dw, float* db) {
+  __shared__ float red[4 * 4 * C];
+  const size_t npix = (size_t)B * R * R;
+  float acc[4 * C];
+#pragma unroll
+  for (int q = 0; q < 4 * C; ++q) acc[q] = 0.f;
+  for (size_t pp = blockIdx.x * (size_t)blockDim.x + threadIdx.x; pp < npix;
+       pp += (size_t)gridDim.x * blockDim.x) {
+    const int px = (int)(pp % R), py = (int)((pp / R) % R), bi = (int)(pp / ((size_t)R * R));
+    float iv[3];
+    img_in3(img, bi, R, py, px, down, iv);
+#pragma unroll
+    for (int o = 0; o < C; o += 4) {
+      float v[4];
+      Ty<T>::ld4(gz + pp * gz_cs + o, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[(o + j) * 3 + 0] += v[j] * iv[0];
+        acc[(o + j) * 3 + 1] += v[j] * iv[1];
+        acc[(o + j) * 3 + 2] += v[j] * iv[2];
+        acc[3 * C + o + j] += v[j];
+      }
+    }
+  }
+  block_reduce_atomic<4 * C, 3 * C>(acc, red, dw, db, c);
+}
+
 __global__ void img_fade_kernel(int B, int C, int R, const float* x, float alpha, float* out) {
   const size_t n = (size_t)B * C * R * R;
   GRID_STRIDE(i, n) {
@@ -531,6 +623,42 @@ __global__ void linear_dgrad_kernel(pg_linear_desc d, const void* gy, const floa
     const size_t xi = LinIO<T>::xidx(d, b, k);
     if (d.flags & PG_LIN_MASK) s *= lmask_f(LinIO<T>::ldx(d, aux, xi), d.slope);
     LinIO<T>::stx(d, gx, xi, s);
+  }
+}
+
+// linear input-gradient: block = 64 k (one per lane) x 4 waves splitting N; B in chunks of 16
+template <typename T>
+__global__ void linear_dgrad_kernel2(pg_linear_desc d, const void* gy, const float* w,
+                                     const void* aux, void* gx) {
+  __shared__ float red[4][16][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int n0 = (d.N * wid) / 4, n1 = (d.N * (wid + 1)) / 4;
+  for (int b0 = 0; b0 < d.B; b0 += 16) {
+    float acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+    if (k < d.K)
+      for (int n = n0; n < n1; ++n) {
+        const float wv = w[(size_t)n * d.K + k];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          if (b0 + q < d.B) acc[q] += wv * LinIO<T>::ldy(d, gy, LinIO<T>::yidx(d, b0 + q, n));
+      }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[wid][q][lane] = acc[q];
+    __syncthreads();
+    for (int q = wid; q < 16; q += 4) {
+      const int b = b0 + q;
+      if (b < d.B && k < d.K) {
+        float sacc = red[0][q][lane] + red[1][q][lane] + red[2][q][lane] + red[3][q][lane];
+        sacc *= d.scale;
+        const size_t xi = LinIO<T>::xidx(d, b, k);
+        if (d.flags & PG_LIN_MASK) sacc *= lmask_f(LinIO<T>::ldx(d, aux, xi), d.slope);
+        LinIO<T>::stx(d, gx, xi, sacc);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -937,9 +1065,18 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     int ppb = 1024;
     int blocks = (int)((npix + ppb - 1) / ppb);
     if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
-    if (dw)
-      hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
-                         0, gimg, dw, db, ppb);
+    if (dw) {
+      const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+      if (C == 16)
+        hipLaunchKernelGGL((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
+                           gimg, dw, db);
+      else if (C == 32)
+        hipLaunchKernelGGL((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
+                           gimg, dw, db);
+      else
+        hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
+                           0, gimg, dw, db, ppb);
+    }
   }
   if (xp) {
     const int Rp = R / 2;
@@ -952,9 +1089,18 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     int ppb = 1024;
     int blocks = (int)((npix + ppb - 1) / ppb);
     if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
-    if (dwp)
-      hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
-                         fp, 1, gimg, dwp, dbp, ppb);
+    if (dwp) {
+      const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+      if (Cp == 16)
+        hipLaunchKernelGGL((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
+                           1, gimg, dwp, dbp);
+      else if (Cp == 32)
+        hipLaunchKernelGGL((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
+                           1, gimg, dwp, dbp);
+      else
+        hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
+                           fp, 1, gimg, dwp, dbp, ppb);
+    }
   }
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1012,12 +1158,28 @@ int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, 
     int ppb = 1024;
     int blocks = (int)((npix + ppb - 1) / ppb);
     if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
-    if (dtype == PG_F32)
-      hipLaunchKernelGGL(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C, img,
-                         down, c, gz_cs, (const float*)gz, dw, db, ppb);
-    else
-      hipLaunchKernelGGL(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
-                         img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
+    const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
+    if (dtype == PG_F32) {
+      if (C == 16)
+        hipLaunchKernelGGL((from_rgb_wgrad_small<float, 16>), dim3(gb), dim3(256), 0, st, B, R, img,
+                           down, c, gz_cs, (const float*)gz, dw, db);
+      else if (C == 32)
+        hipLaunchKernelGGL((from_rgb_wgrad_small<float, 32>), dim3(gb), dim3(256), 0, st, B, R, img,
+                           down, c, gz_cs, (const float*)gz, dw, db);
+      else
+        hipLaunchKernelGGL(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C,
+                           img, down, c, gz_cs, (const float*)gz, dw, db, ppb);
+    } else {
+      if (C == 16)
+        hipLaunchKernelGGL((from_rgb_wgrad_small<bf16_t, 16>), dim3(gb), dim3(256), 0, st, B, R,
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
+      else if (C == 32)
+        hipLaunchKernelGGL((from_rgb_wgrad_small<bf16_t, 32>), dim3(gb), dim3(256), 0, st, B, R,
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
+      else
+        hipLaunchKernelGGL(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
+    }
   }
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1051,7 +1213,9 @@ int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const fl
   PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_dgrad: MASK without aux");
   const size_t n = (size_t)d->B * d->K;
   hipStream_t st = (hipStream_t)stream;
-  DT_DISPATCH(dtype, linear_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, *d, gy, w, aux, gx);
+  (void)n;
+  DT_DISPATCH(dtype, linear_dgrad_kernel2, dim3(pg_cdiv(d->K, 64)), dim3(256), 0, st, *d, gy, w, aux,
+              gx);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1072,10 +1236,10 @@ int pg_mbstd_fwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y
   const int G = mbstd_group(B);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(mbstd_fwd_kernel<float>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+    hipLaunchKernelGGL(mbstd_fwd_kernel<float>, dim3(B / G), dim3(1024), 0, st, B, HW, C, x_cs,
                        (const float*)x, y_cs, (float*)y);
   else
-    hipLaunchKernelGGL(mbstd_fwd_kernel<bf16_t>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+    hipLaunchKernelGGL(mbstd_fwd_kernel<bf16_t>, dim3(B / G), dim3(1024), 0, st, B, HW, C, x_cs,
                        (const bf16_t*)x, y_cs, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1088,14 +1252,14 @@ template <typename T>
 static void mbstd_bwd_launch(int B, int HW, int C, int x_cs, const void* x, int y_cs, const void* gy,
                              void* gx, hipStream_t st) {
   const int G = mbstd_group(B);
-  hipLaunchKernelGGL(mbstd_bwd_kernel<T>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs,
+  hipLaunchKernelGGL(mbstd_bwd_kernel<T>, dim3(B / G), dim3(1024), 0, st, B, HW, C, x_cs,
                      (const T*)x, y_cs, (const T*)gy, (T*)gx);
 }
 template <typename T>
 static void mbstd_r1_launch(int B, int HW, int C, int x_cs, const void* x, const void* a, int y_cs,
                             const void* gy, void* tout, void* inj, hipStream_t st) {
   const int G = mbstd_group(B);
-  hipLaunchKernelGGL(mbstd_r1_kernel<T>, dim3(B / G), dim3(256), 0, st, B, HW, C, x_cs, (const T*)x,
+  hipLaunchKernelGGL(mbstd_r1_kernel<T>, dim3(B / G), dim3(1024), 0, st, B, HW, C, x_cs, (const T*)x,
                      (const T*)a, y_cs, (const T*)gy, (T*)tout, (T*)inj);
 }
 
