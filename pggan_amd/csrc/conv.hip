@@ -22,8 +22,6 @@
 
 namespace {
 
-constexpr int CONV_MAXV = 16;   // max staged 16-byte vectors per thread per chunk
-
 struct ConvParams {
   const void* x;
   const void* w;
@@ -91,7 +89,7 @@ struct Frag<float> {
   }
 };
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR>
 __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
@@ -138,12 +136,12 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   // the weight slab (element offset in x / w without the chunk's channel base, -1 = zero
   // fill) and their LDS byte offsets.  Each chunk is then fetched into registers one
   // chunk ahead (issued before the MFMAs of the current chunk, written to LDS after).
-  int soff[CONV_MAXV], loff[CONV_MAXV];
+  int soff[MAXV], loff[MAXV];
   unsigned wmask = 0;
   const int nhv = npix_halo * vpp;
   const int ntot = nhv + BN * ntap_pad * vpp;
 #pragma unroll
-  for (int j = 0; j < CONV_MAXV; ++j) {
+  for (int j = 0; j < MAXV; ++j) {
     const int i = tid + 256 * j;
     soff[j] = -1;
     loff[j] = -1;
@@ -169,10 +167,10 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   }
   const T* xs = reinterpret_cast<const T*>(p.x);
   const T* wsrc = reinterpret_cast<const T*>(p.w);
-  u32x4_t buf[CONV_MAXV];
+  u32x4_t buf[MAXV];
   auto prefetch = [&](int c0) {
 #pragma unroll
-    for (int j = 0; j < CONV_MAXV; ++j) {
+    for (int j = 0; j < MAXV; ++j) {
       buf[j] = u32x4_t{0u, 0u, 0u, 0u};
       if (soff[j] >= 0) {
         const T* base = ((wmask >> j) & 1u) ? wsrc : xs;
@@ -187,7 +185,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   for (int ch = ch_begin; ch < ch_end; ++ch) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < CONV_MAXV; ++j)
+    for (int j = 0; j < MAXV; ++j)
       if (loff[j] >= 0) *reinterpret_cast<u32x4_t*>(smem + loff[j]) = buf[j];
     __syncthreads();
     if (ch + 1 < ch_end) prefetch((ch + 1) * p.CK);
@@ -206,9 +204,113 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
         Frag<T> afr;
         afr.load(halo + hoff[mt] + toff);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) Frag<T>::mma(afr, bfr[nt], acc[mt][nt]);
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (TR)
+            Frag<T>::mma(bfr[nt], afr, acc[mt][nt]);   // D[cout][pixel]
+          else
+            Frag<T>::mma(afr, bfr[nt], acc[mt][nt]);   // D[pixel][cout]
+        }
       }
     }
+  }
+
+  if constexpr (TR) {
+    // ---- direct epilogue: lane holds 4 consecutive output channels of one pixel, so a
+    // wave-instruction writes 16 pixels x 4 lane-groups x 8 B = whole pixel rows
+    const bool has_bias = !p.ws && (p.flags & PG_CONV_BIAS) != 0;
+    const bool do_lrelu = !p.ws && (p.flags & PG_CONV_LRELU) != 0;
+    const bool do_mask = (p.flags & PG_CONV_MASK) != 0;
+    const bool do_acc = (p.flags & PG_CONV_ACCUM) != 0;
+    const bool pool = !p.ws && (p.flags & PG_CONV_POOL) != 0;
+    T* y = reinterpret_cast<T*>(p.y);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = n0 + wn * (BN / WN) + nt * 16 + 4 * g;
+      const bool nok = n < p.cout;
+      float bv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = (has_bias && nok) ? p.bias[n + j] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pm = wm * (BM / WM) + mt * 16 + r;
+        const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+        const int b = b0 + nb;
+        const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[mt][nt][j] + bv[j];
+          if (do_lrelu) v[j] = lrelu_f(v[j], p.slope);
+        }
+        if (p.ws) {
+          if (b < p.B && n < p.cout_p)
+            *reinterpret_cast<f32x4_t*>(p.ws + blockIdx.z * p.slab + pix * p.cout_p + n) =
+                f32x4_t{v[0], v[1], v[2], v[3]};
+          continue;
+        }
+        if (!pool) {
+          if (b < p.B && nok) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] *= p.out_scale;
+            if (do_mask) {
+              float a[4];
+              Ty<T>::ld4(reinterpret_cast<const T*>(p.aux) + pix * p.aux_cs + n, a);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] *= lmask_f(a[j], p.slope);
+            }
+            T* dst = y + pix * p.y_cs + n;
+            if (do_acc) {
+              float o[4];
+              Ty<T>::ld4(dst, o);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] += o[j];
+            }
+            Ty<T>::st4(dst, v);
+          }
+        } else {
+          if (p.y2 && b < p.B && nok && !(p.TW >= 16 && (mt & 1)))
+            Ty<T>::st4(reinterpret_cast<T*>(p.y2) + pix * p.y2_cs + n, v);
+          // 2x2 sum: horizontal partner = lane ^ 1; vertical = lane ^ TW (TW < 16) or the
+          // next 16-pixel subtile (TW == 16, handled when mt is the even row)
+          float h[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) h[j] = v[j] + __shfl_xor(v[j], 1, 64);
+          if (p.TW < 16) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) h[j] += __shfl_xor(h[j], p.TW, 64);
+          } else {
+            if (mt & 1) continue;
+            if (mt + 1 < MT) {
+              float u[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                u[j] = acc[mt + 1][nt][j] + bv[j];
+                if (do_lrelu) u[j] = lrelu_f(u[j], p.slope);
+              }
+              if (p.y2 && b < p.B && nok)
+                Ty<T>::st4(reinterpret_cast<T*>(p.y2) + (pix + p.W) * p.y2_cs + n, u);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) h[j] += u[j] + __shfl_xor(u[j], 1, 64);
+            }
+          }
+          if ((tx & 1) == 0 && (ty & 1) == 0 && b < p.B && nok) {
+            const size_t op = ((size_t)b * (p.H >> 1) + ((ty0 + ty) >> 1)) * (p.W >> 1) +
+                              ((tx0 + tx) >> 1);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) h[j] *= p.out_scale;
+            T* dst = y + op * p.y_cs + n;
+            if (do_acc) {
+              float o[4];
+              Ty<T>::ld4(dst, o);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) h[j] += o[j];
+            }
+            Ty<T>::st4(dst, h);
+          }
+        }
+      }
+    }
+    return;
   }
 
   // ---- epilogue: accumulators -> LDS tile [BM][BN+4] fp32 (bias, lrelu applied)
@@ -769,18 +871,18 @@ __global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scal
   }
 }
 
-void conv_tile_for(int cout, int* BM, int* BN) {
+void conv_tile_for(int cout, int* BM, int* BN, int W = 16) {
   const int cout_p = (cout + 15) & ~15;
   if (cout_p >= 64) { *BM = 128; *BN = 64; }
-  else if (cout_p >= 32) { *BM = 256; *BN = 32; }
-  else { *BM = 256; *BN = 16; }
+  else if (cout_p >= 32) { *BM = W >= 16 ? 256 : 128; *BN = 32; }
+  else { *BM = W >= 16 ? 256 : 128; *BN = 16; }
 }
 
 // split-K factor: spread the channel chunks of small-spatial / wide convs (4x4..16x16 at
 // 512 channels launch only 8..64 output tiles) over enough workgroups to fill the chip
 int conv_splits(const pg_conv_desc* d) {
   int BM, BN;
-  conv_tile_for(d->cout, &BM, &BN);
+  conv_tile_for(d->cout, &BM, &BN, d->W);
   TileCfg tc = pick_tile(d->H, d->W, BM, BN);
   const int cout_p = (d->cout + 15) & ~15;
   const int base = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH) * pg_cdiv(cout_p, BN);
@@ -799,7 +901,7 @@ size_t conv_ws_bytes(const pg_conv_desc* d) {
   return (size_t)sp * d->B * d->H * d->W * ((d->cout + 15) & ~15) * sizeof(float);
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR>
 int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                 const void* aux, void* y, void* y2, void* ws, size_t ws_bytes, hipStream_t st) {
   TileCfg tc = pick_tile(d->H, d->W, BM, BN);
@@ -827,14 +929,15 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.wrowb = p.KS * 32 * (int)sizeof(T) + 16;
   p.halo_bytes = (tc.NB * (tc.TH + 2) * (tc.TW + 2) * p.pixb + 15) & ~15;
   const int main_bytes = p.halo_bytes + BN * p.wrowb;
-  const int epi_bytes = BM * (BN + 4) * 4;
+  const int epi_bytes = TR ? 0 : BM * (BN + 4) * 4;
   const int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   PG_CHECK_ARG(lds <= 160 * 1024, "conv3x3: LDS %d bytes too large", lds);
   {
     const int vpp = p.CK * (int)sizeof(T) / 16;
     const int ntot = tc.NB * (tc.TH + 2) * (tc.TW + 2) * vpp + BN * (p.KS * 32 / p.CK) * vpp;
-    PG_CHECK_ARG(ntot <= 256 * CONV_MAXV, "conv3x3: %d staged vectors exceed %d per block", ntot,
-                 256 * CONV_MAXV);
+    PG_CHECK_ARG(ntot <= 256 * MAXV, "conv3x3: %d staged vectors exceed %d per block", ntot,
+                 256 * MAXV);
+    (void)0;
   }
   int splits = 1;
   const size_t need = conv_ws_bytes(d);
@@ -846,11 +949,11 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
             splits);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN>,
+    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR>), grid, dim3(256), lds, st, p);
   if (splits > 1) {
     const bool pool = (d->flags & PG_CONV_POOL) != 0;
     const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
@@ -862,14 +965,43 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   return PG_OK;
 }
 
+// staged 16-byte vectors per thread for one chunk (halo tile + weight slab)
+template <typename T>
+int conv_vectors_per_thread(const pg_conv_desc* d, int BM, int BN) {
+  TileCfg tc = pick_tile(d->H, d->W, BM, BN);
+  const int cin_p = cinp_of(d->cin);
+  const int ck_max = sizeof(T) == 4 ? 16 : 32;
+  const int CK = cin_p < ck_max ? cin_p : ck_max;
+  const int KS = (9 * CK + 31) / 32;
+  const int vpp = CK * (int)sizeof(T) / 16;
+  const int ntot = tc.NB * (tc.TH + 2) * (tc.TW + 2) * vpp + BN * (KS * 32 / CK) * vpp;
+  return pg_cdiv(ntot, 256);
+}
+
+template <typename T, int BM, int BN>
+int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
+              const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
+  // fewest staging registers that fit -> highest occupancy for the HBM-bound high-res convs
+  const int v = conv_vectors_per_thread<T>(d, BM, BN);
+  if (v <= 4) return launch_conv<T, BM, BN, 4, 1, 4, true>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  if (v <= 8) return launch_conv<T, BM, BN, 4, 1, 8, true>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  return launch_conv<T, BM, BN, 4, 1, 12, true>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+}
+
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                   const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
   int BM, BN;
-  conv_tile_for(d->cout, &BM, &BN);
-  if (BN == 64) return launch_conv<T, 128, 64, 2, 2>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
-  if (BN == 32) return launch_conv<T, 256, 32, 4, 1>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
-  return launch_conv<T, 256, 16, 4, 1>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  conv_tile_for(d->cout, &BM, &BN, d->W);
+  // cout >= 64: [pixel][cout] MFMA + LDS-transposed epilogue; cout <= 32: [cout][pixel]
+  // MFMA with the direct epilogue (whole pixel rows per store instruction)
+  if (BN == 64) return launch_conv<T, 128, 64, 2, 2, 16, false>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  if (BN == 32) {
+    if (BM == 256) return launch_tr<T, 256, 32>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+    return launch_tr<T, 128, 32>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  }
+  if (BM == 256) return launch_tr<T, 256, 16>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  return launch_tr<T, 128, 16>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
 }
 
 }  // namespace

@@ -100,12 +100,19 @@ class ImageFolderDataset:
 
 
 class ProgressiveGAN:
-    """pggan/model.py:11-265."""
+    """pggan/model.py:11-265.
+
+    `ops_factory(dtype)` builds the kernel op set; the default is the HIP library
+    (`pggan_amd._lib.HipOps`).  Tests substitute a CPU double to exercise the host
+    logic (schedule, checkpoints, DP bookkeeping) without a GPU."""
+
+    ops_factory = None
 
     def __init__(self, args, gpu):
         self.args = args
         self.gpu = gpu
         self.device = torch.device("cuda", gpu) if isinstance(gpu, int) else torch.device(gpu)
+        self.G = self.D = None
         self.scale_index = 0
         self.world, self.rank = 1, 0
         self.dtype = torch.bfloat16 if getattr(args, "compute_dtype", "f32") == "bf16" \
@@ -231,7 +238,8 @@ class ProgressiveGAN:
         if key not in self._engines:
             from . import _lib
             self._engines = {}   # one stage at a time: free the previous stage's buffers
-            eng = E.StepEngine(_lib.HipOps(self.dtype), self.args.depths, self.scale_index, B,
+            factory = type(self).ops_factory or _lib.HipOps
+            eng = E.StepEngine(factory(self.dtype), self.args.depths, self.scale_index, B,
                                self.device, self.args.latent_dim)
             self._engines[key] = eng
         eng = self._engines[key]

@@ -80,13 +80,15 @@ class _MBBlock(nn.Module):
 
 
 _ENGINES = {}
+OPS_FACTORY = None   # tests may substitute a CPU double; default: the HIP library
 
 
 def _engine(ops_dtype, depths, s, B, device):
     from . import _lib
     key = (ops_dtype, tuple(depths), s, B, str(device))
     if key not in _ENGINES:
-        eng = E.StepEngine(_lib.HipOps(ops_dtype), depths, s, B, device)
+        factory = OPS_FACTORY or _lib.HipOps
+        eng = E.StepEngine(factory(ops_dtype), depths, s, B, device)
         eng.hyper = E.Hyper()
         _ENGINES[key] = eng
     return _ENGINES[key]

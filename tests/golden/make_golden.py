@@ -191,8 +191,49 @@ def _store(out, key, t, full):
         out[key + "#norm"] = np.array([np.linalg.norm(flat.astype(np.float64))])
 
 
+SCHEDULE_ARGS = dict(max_step_at_scale=[5, 7, 9, 9], alpha_jump_start=[-1, 2, 3, 1],
+                     alpha_jump_interval=[0, 1, 2, 1], alpha_jump_Ntimes=[0, 3, 2, 4],
+                     depths=[8, 8, 8, 8])
+
+
+def run_schedule(R, n_steps=30):
+    """The reference's progressive schedule (pggan/model.py:141-204 driven as in
+    train.py:27-45) with G/D/solver stubbed: per step (scale_index, alpha_G, alpha_D,
+    alpha_index, next_alpha_jump_step, next_scale_jump_step)."""
+    args = R["Config"].from_yaml(os.path.join(REF, "configs.yaml"))
+    args.isMaster = False
+    for k, v in SCHEDULE_ARGS.items():
+        setattr(args, k, v)
+
+    class Net:
+        alpha = 0
+
+        def add_block(self, d):
+            pass
+
+        def cuda(self):
+            return self
+
+    m = object.__new__(R["ProgressiveGAN"])
+    m.args, m.gpu, m.G, m.D = args, "cpu", Net(), Net()
+    m.reset_solver = lambda: None
+    m.alpha, m.alpha_index, m.scale_index, m.alpha_jump_value = 0, 0, 0, 0
+    m.next_scale_jump_step = args.max_step_at_scale[0]
+    m.next_alpha_jump_step = args.alpha_jump_start[0]
+    rows = []
+    for step in range(n_steps):
+        m.check_jump(step)
+        rows.append([m.scale_index, m.G.alpha, m.D.alpha, m.alpha_index, m.next_alpha_jump_step,
+                     m.next_scale_jump_step])
+    return np.array(rows, np.float64)
+
+
 def main(names):
     R = import_reference()
+    if not names or "schedule" in names:
+        np.savez_compressed(os.path.join(HERE, "schedule.npz"), rows=run_schedule(R),
+                            meta=np.frombuffer(repr(SCHEDULE_ARGS).encode(), dtype=np.uint8))
+        print("schedule: written")
     for (name, depths, s, B, alpha, n_steps, full) in GOLDEN_CONFIGS:
         if names and name not in names:
             continue
