@@ -323,7 +323,7 @@ def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
         for k in P:
             P[k].requires_grad_(False)
     return StepOut(img_real.detach(), img_fake, img_fake_G.detach(), pred_real.detach(),
-                   pred_fake.detach(), pred_fake_G.detach(), float(L_real), float(L_fake),
-                   float(reg), float(L_D), float(L_G),
+                   pred_fake.detach(), pred_fake_G.detach(), L_real.item(), L_fake.item(),
+                   float(reg.detach()) if torch.is_tensor(reg) else float(reg), L_D.item(), L_G.item(),
                    {k: (None if v is None else v.detach()) for k, v in grads_D.items()},
                    {k: (None if v is None else v.detach()) for k, v in grads_G.items()})

@@ -6,6 +6,8 @@ import os
 
 import torch
 
+from .config import cfg_get
+
 
 def save_checkpoint(model, optimizer, name, ckpt_dict):
     ckpt_dict["model"] = {k: v.detach().clone() for k, v in model.state_dict().items()}
@@ -18,12 +20,12 @@ def save_checkpoint(model, optimizer, name, ckpt_dict):
 
 
 def load_checkpoint(args, name, device="cpu"):
-    step = getattr(args, "ckpt_step", None)
+    step = cfg_get(args, "ckpt_step", None)
     step = "latest" if step is None else step
     path = f"{args.save_root}/{args.ckpt_id}/ckpt/{name}_{step}.pt"
     try:
         return torch.load(path, map_location=device, weights_only=True)
     except FileNotFoundError:
-        if getattr(args, "isMaster", False):
+        if cfg_get(args, "isMaster", False):
             print(f"Failed to load checkpoint of {name}.")
         return 0

@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from . import engine as E
+from .config import cfg_get
 from .loss import WGANGPLoss
 from .nets import Discriminator, Generator
 
@@ -115,13 +116,13 @@ class ProgressiveGAN:
         self.G = self.D = None
         self.scale_index = 0
         self.world, self.rank = 1, 0
-        self.dtype = torch.bfloat16 if getattr(args, "compute_dtype", "f32") == "bf16" \
+        self.dtype = torch.bfloat16 if cfg_get(args, "compute_dtype", "f32") == "bf16" \
             else torch.float32
         self.hyper = E.Hyper(lr_G=args.lr_G, lr_D=args.lr_D, beta1=float(args.beta1),
-                             beta2=float(args.beta2), W_adv=float(getattr(args, "W_adv", 1) or 0),
-                             slope_cfg=float(getattr(args, "LReLU_slope", 0.2)),
-                             gp_mode=getattr(args, "gp_mode", "r1"),
-                             W_gp=float(getattr(args, "W_gp", 10)))
+                             beta2=float(args.beta2), W_adv=float(cfg_get(args, "W_adv", 1) or 0),
+                             slope_cfg=float(cfg_get(args, "LReLU_slope", 0.2)),
+                             gp_mode=cfg_get(args, "gp_mode", "r1"),
+                             W_gp=float(cfg_get(args, "W_gp", 10)))
         self._engines = {}
         self._rng_step = 0
         self.global_step = 0
@@ -186,7 +187,7 @@ class ProgressiveGAN:
     def set_dataset(self):
         """pggan/model.py:118-126; falls back to a resident synthetic batch (the benchmark
         setting) when no dataset root exists."""
-        roots = [r for r in (getattr(self.args, "dataset_root_list", None) or []) if os.path.isdir(r)]
+        roots = [r for r in (cfg_get(self.args, "dataset_root_list", None) or []) if os.path.isdir(r)]
         ds = ImageFolderDataset(roots, self.scale_index, seed=self.rank)
         if len(ds) == 0:
             self.train_dataset = None
@@ -285,7 +286,7 @@ class ProgressiveGAN:
         self.alpha_index = 0
         self.next_alpha_jump_step = global_step + self.args.alpha_jump_start[self.scale_index]
         self.alpha_jump_value = 1 / self.args.alpha_jump_Ntimes[self.scale_index]
-        if getattr(self.args, "isMaster", False):
+        if cfg_get(self.args, "isMaster", False):
             print("alpha and alpha_index are initialized to 0")
             print(f"next_alpha_jump_step is set to {self.next_alpha_jump_step}")
             print(f"alpha_jump_value is set to {self.alpha_jump_value}")
@@ -299,7 +300,7 @@ class ProgressiveGAN:
         self._broadcast_params()
         self.reset_solver()
         self.reset_alpha(global_step)
-        if getattr(self.args, "isMaster", False):
+        if cfg_get(self.args, "isMaster", False):
             print(f"\nNOW global_step is {global_step}")
             print(f"scale_index is updated to {self.scale_index}")
             print(f"next_scale_jump_step is {self.next_scale_jump_step}")
@@ -315,7 +316,7 @@ class ProgressiveGAN:
             self.next_alpha_jump_step = 0
         else:
             self.next_alpha_jump_step = global_step + self.args.alpha_jump_interval[self.scale_index]
-        if getattr(self.args, "isMaster", False):
+        if cfg_get(self.args, "isMaster", False):
             print(f"\nNOW global_step is {global_step}")
             print(f"alpha_index is updated to {self.alpha_index}")
             print(f"next_alpha_jump_step is {self.next_alpha_jump_step}")

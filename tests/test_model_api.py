@@ -1,0 +1,210 @@
+"""Host-side API of the drop-in (pggan_amd.nets / pggan_amd.model) on CPU.
+
+The kernels are replaced by the CPU test double (tests/cpu_ops.py) through the
+`ops_factory` / `OPS_FACTORY` seams, so this checks the reference interface
+itself: module state_dict keys and shapes (pggan/nets.py), the progressive
+schedule against the reference's own schedule run (tests/golden/schedule.npz,
+made by tests/golden/make_golden.py from pggan/model.py:141-204), checkpoint
+round trips in the reference file layout (lib/checkpoint.py), and that
+ProgressiveGAN.train_step is the reference step (oracle, pggan/model.py:206-255).
+"""
+import ast
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gen_inputs import TINY_DEPTHS
+from golden_utils import GOLDEN, rel_l2
+
+from cpu_ops import CpuOps
+from oracle import pggan_oracle as O
+from pggan_amd import engine as E
+from pggan_amd import nets
+from pggan_amd.config import Config
+from pggan_amd.model import ProgressiveGAN
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _cpu_ops(monkeypatch):
+    monkeypatch.setattr(ProgressiveGAN, "ops_factory", staticmethod(CpuOps))
+    monkeypatch.setattr(nets, "OPS_FACTORY", CpuOps)
+    nets._ENGINES.clear()
+
+
+def make_args(tmp_path, **over):
+    a = Config.from_yaml(os.path.join(ROOT, "pggan_amd", "default_config.yaml"))
+    a.update(depths=list(TINY_DEPTHS), batch_per_gpu=4, compute_dtype="f32",
+             save_root=str(tmp_path), run_id="t", isMaster=False, dataset_root_list=[])
+    a.update(over)
+    return a
+
+
+def fresh_model(args):
+    m = ProgressiveGAN(args, "cpu")
+    m.initialize_models()
+    m.set_optimizers()
+    m.set_dataset()
+    m.set_data_iterator()
+    m.set_loss_collector()
+    m.scale_index = 0
+    m.alpha_index = 0
+    m.alpha_jump_value = 0
+    m.next_scale_jump_step = args.max_step_at_scale[0]
+    m.next_alpha_jump_step = args.alpha_jump_start[0]
+    return m
+
+
+@pytest.mark.parametrize("s", [0, 1, 2, 3])
+def test_state_dict_matches_reference_layout(s):
+    """Key order and shapes == the reference state_dict (oracle shapes are cited against
+    pggan/nets.py and pinned by the golden fixtures' gradient keys)."""
+    G = nets.Generator(512, TINY_DEPTHS[0])
+    D = nets.Discriminator(TINY_DEPTHS[0], apply_minibatch_norm=True)
+    for i in range(1, s + 1):
+        G.add_block(TINY_DEPTHS[i])
+        D.add_block(TINY_DEPTHS[i])
+    g = [(k, tuple(v.shape)) for k, v in G.state_dict().items()]
+    d = [(k, tuple(v.shape)) for k, v in D.state_dict().items()]
+    assert g == [(k, tuple(v)) for k, v in O.g_param_shapes(TINY_DEPTHS, s)]
+    assert d == [(k, tuple(v)) for k, v in O.d_param_shapes(TINY_DEPTHS, s)]
+
+
+def test_unsupported_switches_raise():
+    with pytest.raises(NotImplementedError):
+        nets.Generator(512, 8, equalized_lr=False)
+    with pytest.raises(NotImplementedError):
+        nets.Discriminator(8, apply_minibatch_norm=False)
+
+
+def test_schedule_matches_reference(tmp_path):
+    z = np.load(os.path.join(GOLDEN, "schedule.npz"), allow_pickle=False)
+    sched = ast.literal_eval(bytes(z["meta"]).decode())
+    ref = z["rows"]
+    args = make_args(tmp_path, batch_per_gpu=2, **sched)
+    m = fresh_model(args)
+    rows = []
+    for step in range(ref.shape[0]):
+        m.check_jump(step)
+        rows.append([m.scale_index, m.G.alpha, m.D.alpha, m.alpha_index, m.next_alpha_jump_step,
+                     m.next_scale_jump_step])
+        # the nets grow with the schedule
+        assert len(m.G.blocks) == m.scale_index and len(m.D.blocks) == m.scale_index
+    np.testing.assert_allclose(np.array(rows, np.float64), ref, rtol=0, atol=1e-12)
+
+
+def test_train_step_is_reference_step(tmp_path):
+    """One ProgressiveGAN.train_step at stage 1, alpha 0.5 == oracle train_step on the
+    same parameters, reals and latents (latents read back from the model)."""
+    args = make_args(tmp_path)
+    m = fresh_model(args)
+    m.change_scale(0)
+    m.G.alpha = m.D.alpha = 0.5
+    PG0 = {k: v.detach().clone() for k, v in m.G.state_dict().items()}
+    PD0 = {k: v.detach().clone() for k, v in m.D.state_dict().items()}
+    img_real, img_fake = m.train_step()
+    real = m.synthetic.clone()
+    z1, z2 = m._z[0].clone(), m._z[1].clone()
+    ref = O.train_step(PG0, PD0, O.AdamState(args.lr_G), O.AdamState(args.lr_D), real, z1, z2,
+                       1, 0.5, 0.5)
+    L = m.loss_collector.loss_dict
+    assert abs(L["L_D_real"] - round(ref.L_D_real, 4)) <= 2e-4
+    assert abs(L["L_D_fake"] - round(ref.L_D_fake, 4)) <= 2e-4
+    assert abs(L["L_G"] - round(ref.L_G, 4)) <= 2e-4
+    assert rel_l2(img_real.numpy(), ref.img_real.numpy()) < 1e-6
+    assert rel_l2(img_fake.numpy(), ref.img_fake_G.numpy()) < 1e-4
+    for k, g in ref.grads_D.items():
+        if g is None:
+            continue
+        got = dict(m.D.named_parameters())[k].grad
+        assert rel_l2(got.numpy(), g.numpy()) < 1e-3, k
+    # parameters after both Adam steps
+    for k, p in PD0.items():
+        assert rel_l2(dict(m.D.named_parameters())[k].detach().numpy(), p.numpy()) < 1e-5, k
+
+
+def test_checkpoint_round_trip(tmp_path):
+    """save_checkpoint -> load_checkpoint (reference paths/keys, weights_only load) restores
+    parameters, Adam moments and schedule scalars; the next step is then identical."""
+    args = make_args(tmp_path, max_step_at_scale=[2, 5, 5], alpha_jump_start=[-1, 0, 0],
+                     alpha_jump_interval=[0, 1, 1], alpha_jump_Ntimes=[0, 4, 4])
+    m = fresh_model(args)
+    for step in range(4):
+        m.check_jump(step)
+        m.train_step()
+    m.save_checkpoint(3)
+    ck = os.path.join(str(tmp_path), "t", "ckpt")
+    assert sorted(os.listdir(ck)) == ["D_3.pt", "D_latest.pt", "G_3.pt", "G_latest.pt"]
+    sd = torch.load(os.path.join(ck, "G_latest.pt"), weights_only=True)
+    for k in ("args", "global_step", "alpha_G", "alpha_D", "alpha_index", "alpha_jump_value",
+              "next_alpha_jump_step", "scale_index", "next_scale_jump_step", "model",
+              "optimizer"):
+        assert k in sd, k
+    assert list(sd["model"].keys()) == list(m.G.state_dict().keys())
+
+    args2 = make_args(tmp_path, ckpt_id="t", max_step_at_scale=[2, 5, 5],
+                      alpha_jump_start=[-1, 0, 0], alpha_jump_interval=[0, 1, 1],
+                      alpha_jump_Ntimes=[0, 4, 4])
+    m2 = ProgressiveGAN(args2, "cpu")
+    m2.initialize_models()
+    m2.set_optimizers()
+    m2.set_dataset()
+    m2.set_data_iterator()
+    m2.set_loss_collector()
+    m2.load_checkpoint()
+    assert (m2.scale_index, m2.G.alpha, m2.alpha_index, m2.next_alpha_jump_step,
+            m2.next_scale_jump_step, m2.global_step) == \
+        (m.scale_index, m.G.alpha, m.alpha_index, m.next_alpha_jump_step,
+         m.next_scale_jump_step, 3)
+    for a, b in ((m.G, m2.G), (m.D, m2.D)):
+        for (k, p), (k2, p2) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert k == k2 and torch.equal(p, p2), k
+    assert torch.equal(m.fpD.m, m2.fpD.m) and torch.equal(m.fpD.v, m2.fpD.v)
+    assert m.fpD.step == m2.fpD.step and m.fpG.step == m2.fpG.step
+    # one more step on both (same latents, same reals) gives the same parameters
+    m2._rng_step = m._rng_step
+    m.train_step()
+    m2.train_step()
+    for a, b in ((m.G, m2.G), (m.D, m2.D)):
+        for (k, p), (_, p2) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert torch.allclose(p, p2, rtol=0, atol=0), k
+
+
+def test_product_path_requires_hip_library(monkeypatch):
+    """Without the seam the model binds the HIP library, which refuses CPU tensors: no
+    silent CPU fallback."""
+    monkeypatch.setattr(ProgressiveGAN, "ops_factory", None)
+    from pggan_amd import _lib
+    try:
+        ops = _lib.HipOps(torch.float32)
+    except (OSError, RuntimeError):
+        return   # library absent: loading already fails loudly
+    with pytest.raises((RuntimeError, ValueError, AssertionError)):
+        ops.pixnorm(torch.zeros(4, 8), torch.zeros(4, 8), 8)
+
+
+class _RefStyleConfig:
+    """Behaves like the reference's lib/config.py Config: attribute reads of missing keys
+    raise KeyError (lib/config.py:26-27), not AttributeError."""
+
+    def __init__(self, d):
+        self.__dict__.update(d)
+
+    def __getattr__(self, k):
+        return self.__dict__[k]
+
+    def __setitem__(self, k, v):
+        self.__dict__[k] = v
+
+
+def test_accepts_reference_config_object(tmp_path):
+    d = dict(make_args(tmp_path))
+    for k in ("compute_dtype", "gp_mode", "W_gp"):   # keys the reference config lacks
+        d.pop(k)
+    m = fresh_model(_RefStyleConfig(d))
+    assert m.dtype == torch.float32 and m.hyper.gp_mode == "r1"
+    m.train_step()
+    assert np.isfinite(m.loss_collector.loss_dict["L_D"])
