@@ -27,6 +27,7 @@ METRIC = "images/sec (G+D+GP step) at 1024×1024 bs=4/GPU, 1/2/4/8 MI355X"
 PAPER_DEPTHS = [512, 512, 512, 512, 256, 128, 64, 32, 16]
 # dense peaks, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}
+PEAK_HBM_GBS = 8000.0
 
 
 def parse():
@@ -44,12 +45,29 @@ def parse():
     return p.parse_args()
 
 
+def conv_bytes(x, wpk, y, kw):
+    """Algorithmic HBM bytes of one conv3x3 launch: input (at its stored resolution), output
+    (read too when accumulating), the mask operand, the second output, packed weights."""
+    B, H, W, fl = kw["B"], kw["H"], kw["W"], kw["flags"]
+    es = y.element_size()
+    hin = H // 2 if fl & 1 else H
+    ho = H // 2 if fl & 16 else H
+    n = B * hin * (W // 2 if fl & 1 else W) * x.shape[-1]
+    n += B * ho * (W // 2 if fl & 16 else W) * y.shape[-1] * (2 if fl & 32 else 1)
+    if kw.get("aux") is not None:
+        n += B * H * W * kw["aux"].shape[-1]
+    if kw.get("y2") is not None:
+        n += B * ho * (W // 2 if fl & 16 else W) * kw["y2"].shape[-1]
+    return n * es + wpk.numel() * wpk.element_size()
+
+
 class KernelTimer:
     """HIP events around every conv launch (fwd/dgrad/tangent kernel and wgrad kernel),
     recorded on the stream the kernels run on; FLOPs are the algorithmic MAC count x2
     of the logical channels."""
 
-    def __init__(self, ops):
+    def __init__(self, ops, dtype):
+        self.dtype = dtype
         self.rec = {"conv3x3": [], "wgrad3x3": []}
         self.shapes = []
         self.on = False
@@ -63,8 +81,10 @@ class KernelTimer:
             f_conv(x, wpk, y, **kw)
             b.record()
             fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
-            self.rec["conv3x3"].append((a, b, fl))
-            self.shapes.append(("conv3x3", kw["H"], kw["cin"], kw["cout"], kw["flags"], a, b, fl))
+            by = conv_bytes(x, wpk, y, kw)
+            self.rec["conv3x3"].append((a, b, fl, by))
+            self.shapes.append(("conv3x3", kw["H"], kw["cin"], kw["cout"], kw["flags"], a, b, fl,
+                                by))
 
         def conv_wgrad(x, gz, dw, **kw):
             if not self.on:
@@ -74,34 +94,49 @@ class KernelTimer:
             f_wg(x, gz, dw, **kw)
             b.record()
             fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
-            self.rec["wgrad3x3"].append((a, b, fl))
+            hin = kw["H"] // 2 if kw["ups"] else kw["H"]
+            by = (kw["B"] * hin * hin * x.shape[-1] + kw["B"] * kw["H"] * kw["W"] * gz.shape[-1]) \
+                * x.element_size() + 2 * dw.numel() * 4
+            self.rec["wgrad3x3"].append((a, b, fl, by))
             self.shapes.append(("wgrad3x3", kw["H"], kw["cin"], kw["cout"], int(kw["ups"]), a, b,
-                                fl))
+                                fl, by))
 
         ops.conv3x3, ops.conv_wgrad = conv3x3, conv_wgrad
 
     def per_shape(self, steps):
         agg = {}
-        for k, H, ci, co, fl, a, b, f in self.shapes:
+        for k, H, ci, co, fl, a, b, f, by in self.shapes:
             key = (k, H, ci, co, fl)
-            t = agg.setdefault(key, [0.0, 0.0, 0])
+            t = agg.setdefault(key, [0.0, 0.0, 0, 0.0])
             t[0] += a.elapsed_time(b)
             t[1] += f
             t[2] += 1
+            t[3] += by
         rows = sorted(agg.items(), key=lambda kv: -kv[1][0])
         return [dict(kernel=k[0], H=k[1], cin=k[2], cout=k[3], flags=k[4],
                      ms_per_step=round(v[0] / steps, 3), tflops=round(v[1] / (v[0] * 1e-3) / 1e12, 1),
+                     gbps=round(v[3] / (v[0] * 1e-3) / 1e9, 1),
                      calls_per_step=v[2] // steps) for k, v in rows]
+
+    def peak_key(self, fam):
+        # the f32 path and the f32-MFMA wgrad kernel run at the f32 MFMA rate
+        return "f32" if self.dtype == "f32" else "bf16"
 
     def summary(self):
         out = {}
         for k, lst in self.rec.items():
             if not lst:
                 continue
-            ms = sum(a.elapsed_time(b) for a, b, _ in lst)
-            fl = sum(f for _, _, f in lst)
+            pf = PEAK_TFLOPS[self.peak_key(k)] * 1e12
+            ms = sum(a.elapsed_time(b) for a, b, _, _ in lst)
+            fl = sum(f for _, _, f, _ in lst)
+            by = sum(v for _, _, _, v in lst)
+            # per-launch roofline time: max(flops / MFMA peak, bytes / HBM peak)
+            roof_s = sum(max(f / pf, v / (PEAK_HBM_GBS * 1e9)) for _, _, f, v in lst)
             out[k] = dict(launches=len(lst), total_ms=ms, avg_us=1e3 * ms / len(lst),
-                          flops=fl, tflops=fl / (ms * 1e-3) / 1e12)
+                          flops=fl, bytes=by, tflops=fl / (ms * 1e-3) / 1e12,
+                          gbps=by / (ms * 1e-3) / 1e9, roofline_time_frac=roof_s / (ms * 1e-3),
+                          t_mfma_s=fl / pf, t_hbm_s=by / (PEAK_HBM_GBS * 1e9))
         return out
 
 
@@ -113,6 +148,24 @@ def init_params(E, depths, s, device, rank_seed):
     fpG = E.FlatParams(gsh, E.dead_params("G", s), device, init(gsh))
     fpD = E.FlatParams(dsh, E.dead_params("D", s), device, init(dsh))
     return fpG, fpD
+
+
+def pmc_traffic(args, fam):
+    """HBM bytes per launch of `fam` from the newest committed rocprofv3 PMC summary of this
+    same workload (profiles/*_prof_summary.json, written by tools/prof_summary.py from
+    separate --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, gfx950 FETCH x2 correction).
+    PMC counters cannot be read inside the timed run, so this is the profiled twin's value."""
+    import glob
+    key = f"stage{args.stage}_b{args.batch}_{args.dtype}"
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_prof_summary.json")), reverse=True):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        f = d.get("families", {}).get(fam, {})
+        if d.get("config") == key and f.get("hbm_bytes_per_call"):
+            return round(f["hbm_bytes_per_call"]), os.path.relpath(p, ROOT)
+    return None, None
 
 
 def cpu_baseline(args, steps=1):
@@ -159,7 +212,7 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     ops = _lib.HipOps(dtype)
-    timer = None if args.no_kernel_events else KernelTimer(ops)
+    timer = None if args.no_kernel_events else KernelTimer(ops, args.dtype)
     s, B = args.stage, args.batch
     depths = PAPER_DEPTHS
     R = 4 * 2 ** s
@@ -217,14 +270,23 @@ def main():
         if ksum:
             dom = max(ksum, key=lambda k: ksum[k]["total_ms"])
             kd = ksum[dom]
-            peak_key = "f32" if (dom == "wgrad3x3" or args.dtype == "f32") else "bf16"
-            peak = PEAK_TFLOPS[peak_key]
-            roof = dict(bound="mfma", kernel=dom, achieved=round(kd["tflops"], 2), peak=peak,
-                        unit="TFLOP/s", frac=round(kd["tflops"] / peak, 4), traffic=None,
+            hbm = kd["t_hbm_s"] > kd["t_mfma_s"]
+            if hbm:
+                ach, peak, unit = kd["gbps"], PEAK_HBM_GBS, "GB/s"
+            else:
+                ach, peak, unit = kd["tflops"], PEAK_TFLOPS[timer.peak_key(dom)], "TFLOP/s"
+            traffic, tsrc = pmc_traffic(args, dom)
+            roof = dict(bound="hbm" if hbm else "mfma", kernel=dom, achieved=round(ach, 2),
+                        peak=peak, unit=unit, frac=round(ach / peak, 4), traffic=traffic,
+                        traffic_source=tsrc,
+                        algorithmic_bytes_per_launch=round(kd["bytes"] / kd["launches"]),
+                        flops_per_launch=round(kd["flops"] / kd["launches"]),
                         launches_per_step=kd["launches"] // args.steps,
                         avg_launch_us=round(kd["avg_us"], 2),
+                        roofline_time_frac=round(kd["roofline_time_frac"], 4),
                         kernels={k: dict(total_ms_per_step=round(v["total_ms"] / args.steps, 3),
-                                         tflops=round(v["tflops"], 2),
+                                         tflops=round(v["tflops"], 2), gbps=round(v["gbps"], 1),
+                                         roofline_time_frac=round(v["roofline_time_frac"], 4),
                                          launches_per_step=v["launches"] // args.steps)
                                  for k, v in ksum.items()})
         cpu = None

@@ -29,6 +29,19 @@ for step in "$@"; do
           --cpu-baseline off --no-kernel-events ) > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -n 3 gpurun_out/prof.log
       if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    pmc)
+      ROOT=$(pwd)
+      export TMPDIR=/tmp
+      for c in FETCH_SIZE WRITE_SIZE; do
+        ( cd /tmp && timeout -k 10 900 rocprofv3 --pmc $c --output-format csv \
+            -d "$ROOT/gpurun_out/pmc_$c" -o run -- python "$ROOT/bench.py" --steps 1 --warmup 1 \
+            --cpu-baseline off --no-kernel-events ) > gpurun_out/pmc_$c.log 2>&1
+        rc=$?; echo "pmc $c rc=$rc"; tail -n 3 gpurun_out/pmc_$c.log
+        if [ $rc -ne 0 ]; then exit $rc; fi
+      done
+      python tools/prof_summary.py gpurun_out/prof --fetch gpurun_out/pmc_FETCH_SIZE \
+        --write gpurun_out/pmc_WRITE_SIZE \
+        -o gpurun_out/prof_summary.json > /dev/null ;;
     shapes) PG_BENCH_SHAPES=gpurun_out/shapes.json run shapes 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -1,0 +1,84 @@
+"""Micro-benchmark of single conv / wgrad launches at bench shapes (GPU only).
+
+    python tools/kbench.py [--B 4] [--iters 20] SPEC [SPEC ...]
+    SPEC = c:H:cin:cout:flags   conv3x3 (flags as in include/pggan_hip.h; H = output size
+                                 before pooling)
+           w:H:cin:cout:ups     conv3x3 weight gradient (with fused bias grad)
+Prints one line per spec: avg us per launch, TFLOP/s and the GB/s of the minimal bytes.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pggan_amd import _lib  # noqa: E402
+from pggan_amd.engine import cinp  # noqa: E402
+
+
+def r8(c):
+    return (c + 7) // 8 * 8
+
+
+def run(ops, spec, B, iters):
+    kind, H, cin, cout, fl = spec.split(":")
+    H, cin, cout, fl = int(H), int(cin), int(cout), int(fl)
+    dev, bf = "cuda", torch.bfloat16
+    cp = cinp(cin)
+    g = torch.Generator(device=dev).manual_seed(0)
+    if kind == "c":
+        Hin = H // 2 if fl & 1 else H
+        x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
+        wpk = torch.randn(ops.packed_elems(0, cout, cin), device=dev, generator=g).to(bf) * 0.05
+        Ho = H // 2 if fl & 16 else H
+        y = torch.empty(B, Ho, Ho, cinp(cout), device=dev, dtype=bf)
+        aux = torch.randn(B, H, H, r8(cout), device=dev, generator=g).to(bf) if fl & 8 else None
+        bias = torch.zeros(cout, device=dev) if fl & 2 else None
+        nb = ops.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
+        ws = torch.empty(max(nb // 4, 1), device=dev) if nb else None
+
+        def f():
+            ops.conv3x3(x, wpk, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=fl, bias=bias,
+                        aux=aux, ws=ws, out_scale=0.25 if fl & 16 else 1.0)
+        byts = x.numel() * 2 + y.numel() * 2 + (aux.numel() * 2 if aux is not None else 0)
+    else:
+        Hin = H // 2 if fl else H
+        x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
+        gz = torch.randn(B, H, H, r8(cout), device=dev, generator=g).to(bf)
+        dw = torch.zeros(cout, cin, 3, 3, device=dev)
+        db = torch.zeros(cout, device=dev)
+
+        def f():
+            ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=bool(fl), scale=1.0,
+                           db=db)
+        byts = x.numel() * 2 + gz.numel() * 2
+    for _ in range(3):
+        f()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(iters):
+        f()
+    b.record()
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / iters
+    flops = 2.0 * B * H * H * 9 * cin * cout
+    print(f"{spec:24s} {us:9.1f} us  {flops / us / 1e6:8.1f} TF/s  {byts / us / 1e3:8.1f} GB/s",
+          flush=True)
+    return us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("specs", nargs="+")
+    a = ap.parse_args()
+    ops = _lib.HipOps(torch.bfloat16)
+    for s in a.specs:
+        run(ops, s, a.B, a.iters)
+
+
+if __name__ == "__main__":
+    main()

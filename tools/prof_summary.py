@@ -1,0 +1,126 @@
+"""Summarise rocprofv3 output of a bench.py run into the kernel families bench.py reports.
+
+    python tools/prof_summary.py <kernel_trace.csv> [--fetch counter_collection.csv]
+                                 [--write counter_collection.csv] [--steps-total N]
+                                 [-o out.json]
+
+Families (same bracketing as bench.py's HIP events):
+  conv3x3  = conv3x3_kernel dispatches + their split-K epilogue dispatches, per conv call
+  wgrad3x3 = wgrad3x3_kernel / wgrad_bf16_kernel dispatches (bias grad fused), per call
+Traffic per call = 2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md "HBM [CDNA4]": gfx950
+FETCH_SIZE reports half of the bytes of wide coalesced reads; WRITE_SIZE is exact for
+16-B stores and float atomics), summed over the family's dispatches / calls.
+"""
+import argparse
+import csv
+import glob
+import os
+import json
+from collections import defaultdict
+
+
+def family(name):
+    if "conv3x3_kernel" in name:
+        return "conv3x3", True
+    if "conv_splitk_epilogue" in name:
+        return "conv3x3", False
+    if "wgrad3x3_kernel" in name or "wgrad_bf16_kernel" in name:
+        return "wgrad3x3", True
+    return None, False
+
+
+def short(name):
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+
+
+def read_trace(path):
+    path = _resolve(path, "kernel_trace.csv")
+    fam = defaultdict(lambda: dict(ns=0, calls=0, dispatches=0))
+    per_kernel = defaultdict(lambda: [0, 0])
+    total = 0
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            n = r["Kernel_Name"]
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            total += d
+            k = per_kernel[short(n)]
+            k[0] += d
+            k[1] += 1
+            fm, is_call = family(n)
+            if fm:
+                fam[fm]["ns"] += d
+                fam[fm]["dispatches"] += 1
+                fam[fm]["calls"] += int(is_call)
+    return fam, per_kernel, total
+
+
+def _resolve(path, suffix):
+    if os.path.isdir(path):
+        hits = sorted(glob.glob(os.path.join(path, "**", "*" + suffix), recursive=True))
+        if not hits:
+            raise SystemExit(f"no *{suffix} under {path}")
+        return hits[0]
+    return path
+
+
+def read_counter(path, counter):
+    path = _resolve(path, "counter_collection.csv")
+    """-> ({family: summed value}, {family: calls}, {short kernel name: [sum, dispatches]})"""
+    out, calls = defaultdict(float), defaultdict(int)
+    per = defaultdict(lambda: [0.0, 0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r.get("Counter_Name") != counter:
+                continue
+            fm, is_call = family(r["Kernel_Name"])
+            v = float(r["Counter_Value"])
+            out[fm or "other"] += v
+            calls[fm or "other"] += int(is_call)
+            k = per[short(r["Kernel_Name"])]
+            k[0] += v
+            k[1] += 1
+    return out, calls, per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("-o", "--out")
+    ap.add_argument("--config", default="stage8_b4_bf16",
+                    help="bench.py workload key the profiled run used (bench.py matches it)")
+    a = ap.parse_args()
+    fam, per_kernel, total = read_trace(a.trace)
+    res = {"config": a.config, "total_kernel_ms": total / 1e6, "families": {},
+           "top_kernels": []}
+    for k, v in fam.items():
+        res["families"][k] = dict(total_ms=v["ns"] / 1e6, calls=v["calls"],
+                                  dispatches=v["dispatches"],
+                                  avg_us_per_call=v["ns"] / 1e3 / max(v["calls"], 1))
+    if a.fetch and a.write:
+        fe, fcalls, fper = read_counter(a.fetch, "FETCH_SIZE")
+        wr, _, wper = read_counter(a.write, "WRITE_SIZE")
+        for k, v in res["families"].items():
+            # FETCH_SIZE / WRITE_SIZE are reported in KiB
+            by = (2.0 * fe.get(k, 0.0) + wr.get(k, 0.0)) * 1024.0
+            v["pmc_calls"] = fcalls.get(k, 0)
+            v["hbm_bytes_per_call"] = by / max(fcalls.get(k, 0), 1)
+        res["pmc_per_kernel_kib"] = {n: dict(fetch_x2=2 * f[0] / f[1],
+                                             write=wper.get(n, [0, 1])[0] / max(wper.get(n, [0, 1])[1], 1),
+                                             dispatches=f[1])
+                                     for n, f in sorted(fper.items(), key=lambda kv: -kv[1][0])[:25]}
+        res["pmc_note"] = ("bytes/call = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 summed over the "
+                           "family's dispatches of the PMC passes / the family's calls; "
+                           "calibrate with adam_kernel: 28 B per parameter (4 fp32 reads, 3 writes)")
+    for n, (ns, c) in sorted(per_kernel.items(), key=lambda kv: -kv[1][0])[:25]:
+        res["top_kernels"].append(dict(kernel=n, total_ms=ns / 1e6, calls=c,
+                                       avg_us=ns / 1e3 / c, pct=100.0 * ns / total))
+    s = json.dumps(res, indent=1)
+    if a.out:
+        open(a.out, "w").write(s)
+    print(s)
+
+
+if __name__ == "__main__":
+    main()
