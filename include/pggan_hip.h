@@ -77,8 +77,12 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
  * and, if db != NULL, the bias gradient db[o] += scale * sum_p gz[p][o] (fused: gz is read
  * once).  desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold
  * PG_CONV_UPS_IN.  bf16: cout and both channel strides must be multiples of 8. */
+/* ws: optional fp32 workspace (>= pg_conv3x3_wgrad_workspace_size bytes).  When the pixel
+ * range is split over workgroups the partial sums go to per-split slabs of ws and a
+ * second kernel adds them into dw/db; NULL or too small -> fp32 atomics per split. */
+size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d);
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, float* db, void* stream);
+                     float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
 /* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
                  void* stream);

@@ -45,7 +45,9 @@ _SIGS = {
     "pg_conv3x3_workspace_size": ([ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
                        _I),
-    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP], _I),
+    "pg_conv3x3_wgrad_workspace_size": ([_I, ctypes.POINTER(ConvDesc)], _SZ),
+    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP],
+                         _I),
     "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
@@ -153,12 +155,19 @@ class HipOps:
         d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, 0, 0.0, 1.0)
         return int(self.lib.pg_conv3x3_workspace_size(ctypes.byref(d)))
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None):
-        self._cuda(x, gz, dw, db)
+    def wgrad_workspace_bytes(self, *, B, H, W, cin, cout, ups=False):
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, CONV_UPS_IN if ups else 0, 0.0, 1.0)
+        return int(self.lib.pg_conv3x3_wgrad_workspace_size(self.dt, ctypes.byref(d)))
+
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None):
+        """ws: optional fp32 workspace (see wgrad_workspace_bytes) for split reductions."""
+        self._cuda(x, gz, dw, db, ws)
         d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0,
                      CONV_UPS_IN if ups else 0, 0.0, 1.0)
+        wsb = ws.numel() * ws.element_size() if ws is not None else 0
         self._chk(self.lib.pg_conv3x3_wgrad(self._dt(gz), ctypes.byref(d), _p(x), _p(gz), scale,
-                                            _p(dw), _p(db), self._s()), "conv3x3_wgrad")
+                                            _p(dw), _p(db), _p(ws), wsb, self._s()),
+                  "conv3x3_wgrad")
 
     def bias_grad(self, g, db, C, scale):
         self._cuda(g, db)

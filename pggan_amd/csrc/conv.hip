@@ -583,13 +583,26 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
 }
 
 // --------------------------------------------------------------------------
-// bf16 weight gradient on v_mfma_f32_16x16x32_bf16.  K = pixels: both operands
-// are staged pixel-major in LDS ([pixel][o] and the [halo pixel][c] tile) and the
-// k-contiguous fragments are read with ds_read_b64_tr_b16 (gfx950 transposed
-// read: 16 lanes fetch a 4-row x 16-column block, lane i receives column i),
-// whose per-lane row addresses also apply the 3x3 tap shift.  A wave owns
-// MO x NC 16x16 (o, c) blocks for all 9 taps; KW waves split the pixel k-steps
-// and are reduced through LDS; one fp32 atomic per (o, c, tap) per workgroup.
+// bf16 weight gradient on v_mfma_f32_16x16x32_bf16.  GEMM view: M = cout,
+// N = 9 taps x cin, K = pixels.  Both operands are staged pixel-major in LDS
+// ([pixel][o] and the [halo pixel][c] tile) and the k-contiguous fragments are
+// read with ds_read_b64_tr_b16 (gfx950 transposed read: 16 lanes fetch a 4-row x
+// 16-column block, lane i receives column i), whose per-lane row addresses also
+// apply the 3x3 tap shift.  A wave owns MO x NC 16x16 (o, c) blocks for all 9
+// taps; KW waves split the pixel k-steps and are reduced through LDS.
+//
+// Pipeline: the global loads of pixel tile t+1 are issued into registers before
+// the MFMAs of tile t (one LDS buffer, two barriers per tile), so every resident
+// workgroup keeps a tile of loads in flight.  The bias gradient is summed from
+// the staged gz registers (no extra LDS pass).
+//
+// Reduction over pixel splits (blockIdx.z), chosen on the host:
+//   WG_DIRECT : one split -> plain coalesced read-modify-write of dw / db
+//   WG_SLABS  : split z writes an fp32 partial slab of the workspace; a second
+//               kernel sums the slabs into dw / db (few, spread atomics)
+//   WG_ATOMIC : no workspace given -> fp32 atomics per (o, c, tap) per split
+// Writes go through a per-wave LDS transpose so that each wave instruction covers
+// contiguous [c][tap] runs of one OIHW row.
 // --------------------------------------------------------------------------
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
@@ -600,11 +613,16 @@ __device__ __forceinline__ bf16x8_t tr_read8(const bf16_t* lo, const bf16_t* hi)
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+enum { WG_DIRECT = 0, WG_SLABS = 1, WG_ATOMIC = 2 };
+
 struct WgBParams {
   const bf16_t* x;
   const bf16_t* gz;
   float* dw;
   float* db;
+  float* ws;       // WG_SLABS: [splits][slab] fp32, slab = cout*cin*9 + cout
+  size_t slab;
+  int mode;
   int B, H, W, Hin, Win;
   int cin, cout, x_cs, gz_cs;
   int ups;
@@ -613,12 +631,21 @@ struct WgBParams {
   int GZS, HS, halo_elems;
 };
 
-constexpr int WGB_BP = 128;
+constexpr int WGB_BP = 128;        // pixels per staged tile
+constexpr int WGB_MAXHALO = 288;   // max halo pixels of a 128-pixel tile (pick_tile, W = 4)
+
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
 template <int MO, int NC, int WMO, int WNC>
-__global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MO >= 4 ? 2 : MO == 2 ? 3 : 4)))
+void wgrad_bf16_kernel(WgBParams p) {
   constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
+  constexpr int GV = BO / 8, HV = BC / 8;
+  constexpr int NGZ = WGB_BP * GV / 256;                  // gz vectors per thread
+  constexpr int NH = (WGB_MAXHALO * HV + 255) / 256;      // halo vectors per thread (max)
+  static_assert(NGZ * 256 == WGB_BP * GV, "gz staging must tile the workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* gzl = reinterpret_cast<bf16_t*>(smem);
   bf16_t* hal = gzl + WGB_BP * p.GZS;
@@ -628,6 +655,7 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
   const int o0 = blockIdx.x * BO, c0 = blockIdx.y * BC;
   const int TW2 = p.TW + 2, HW2 = (p.TH + 2) * TW2;
+  const int nhalo = p.halo_elems * HV;
 
   f32x4_t acc[MO][NC][9];
 #pragma unroll
@@ -637,46 +665,88 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[a][b][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  float bsum = 0.f;   // bias gradient of output channel o0 + tid (c-tile 0 only)
-  const bool do_db = p.db && blockIdx.y == 0 && tid < BO;
-  const int t_begin = blockIdx.z * p.tiles_per_split;
-  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
-  for (int t = t_begin; t < t_end; ++t) {
-    int tt = t;
-    const int tx0 = (tt % p.tiles_x) * p.TW;
-    tt /= p.tiles_x;
-    const int ty0 = (tt % p.tiles_y) * p.TH;
-    tt /= p.tiles_y;
-    const int b0 = tt * p.NB;
-    __syncthreads();
-    constexpr int GV = BO / 8;
-    for (int i = tid; i < WGB_BP * GV; i += 256) {
-      const int pm = i / GV, v = i - pm * GV;
-      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
-      const int b = b0 + nb, o = o0 + 8 * v;
-      u32x4_t val = {0u, 0u, 0u, 0u};
-      if (b < p.B && o < p.cout)
-        val = *reinterpret_cast<const u32x4_t*>(
-            p.gz + (((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx) * p.gz_cs + o);
-      *reinterpret_cast<u32x4_t*>(gzl + pm * p.GZS + 8 * v) = val;
-    }
-    constexpr int HV = BC / 8;
-    for (int i = tid; i < p.halo_elems * HV; i += 256) {
+  const bool do_db = p.db && blockIdx.y == 0;
+  float bs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+
+  // per-thread staging plan (fixed across tiles; TH, TW even so the upsample's floor
+  // shift splits over tile origin + offset): gz element k -> (pixel offset, image),
+  // halo element k -> packed (image, hy, hx, channel vector) or -1
+  int gzrel[NGZ], gznb[NGZ], hpk[NH];
+#pragma unroll
+  for (int k = 0; k < NGZ; ++k) {
+    const int i = tid + k * 256;
+    const int pm = i / GV, v = i - pm * GV;
+    const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+    gzrel[k] = ((nb * p.H + ty) * p.W + tx) * p.gz_cs + 8 * v;
+    gznb[k] = (o0 + 8 * v < p.cout) ? nb : 1 << 20;
+  }
+#pragma unroll
+  for (int k = 0; k < NH; ++k) {
+    const int i = tid + k * 256;
+    hpk[k] = -1;
+    if (i < nhalo) {
       const int hp = i / HV, v = i - hp * HV;
       const int nb = hp / HW2, rem = hp - nb * HW2;
       const int hy = rem / TW2, hx = rem - hy * TW2;
-      const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1, c = c0 + 8 * v;
-      u32x4_t val = {0u, 0u, 0u, 0u};
-      if (b < p.B && c < p.x_cs && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
-        const int sy = p.ups ? (yy >> 1) : yy, sx = p.ups ? (xx >> 1) : xx;
-        val = *reinterpret_cast<const u32x4_t*>(
-            p.x + (((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + c);
+      if (c0 + 8 * v < p.x_cs) hpk[k] = (nb << 24) | (hy << 16) | (hx << 8) | v;
+    }
+  }
+  u32x4_t rg[NGZ], rh[NH];
+  auto load_tile = [&](int t) {
+    const int tx0 = (t % p.tiles_x) * p.TW;
+    int tt = t / p.tiles_x;
+    const int ty0 = (tt % p.tiles_y) * p.TH;
+    const int b0 = (tt / p.tiles_y) * p.NB;
+    const bf16_t* gzt = p.gz + (((size_t)b0 * p.H + ty0) * p.W + tx0) * p.gz_cs + o0;
+#pragma unroll
+    for (int k = 0; k < NGZ; ++k) {
+      rg[k] = u32x4_t{0u, 0u, 0u, 0u};
+      if (b0 + gznb[k] < p.B) rg[k] = *reinterpret_cast<const u32x4_t*>(gzt + gzrel[k]);
+    }
+    const int ys = p.ups ? 1 : 0;
+    const bf16_t* xb = p.x + c0;
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      rh[k] = u32x4_t{0u, 0u, 0u, 0u};
+      const int pk = hpk[k];
+      const int b = b0 + (pk >> 24), yy = ty0 + ((pk >> 16) & 0xff) - 1,
+                xx = tx0 + ((pk >> 8) & 0xff) - 1;
+      if (pk >= 0 && b < p.B && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
+        rh[k] = *reinterpret_cast<const u32x4_t*>(
+            xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff));
+    }
+  };
+
+  const int t_begin = blockIdx.z * p.tiles_per_split;
+  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
+  if (t_begin < t_end) load_tile(t_begin);
+  for (int t = t_begin; t < t_end; ++t) {
+    __syncthreads();   // the previous tile's fragments have been read
+#pragma unroll
+    for (int k = 0; k < NGZ; ++k) {
+      const int i = tid + k * 256;
+      const int pm = i / GV, v = i - pm * GV;
+      *reinterpret_cast<u32x4_t*>(gzl + pm * p.GZS + 8 * v) = rg[k];
+      if (do_db) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bs[2 * e] += bf_lo(rg[k][e]);
+          bs[2 * e + 1] += bf_hi(rg[k][e]);
+        }
       }
-      *reinterpret_cast<u32x4_t*>(hal + hp * p.HS + 8 * v) = val;
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int i = tid + k * 256;
+      if (i < nhalo) {
+        const int hp = i / HV, v = i - hp * HV;
+        *reinterpret_cast<u32x4_t*>(hal + hp * p.HS + 8 * v) = rh[k];
+      }
     }
     __syncthreads();
-    if (do_db)
-      for (int pm = 0; pm < WGB_BP; ++pm) bsum += bf2f(gzl[pm * p.GZS + tid]);
+    if (t + 1 < t_end) load_tile(t + 1);   // in flight during this tile's MFMAs
     for (int ks = wk; ks < WGB_BP / 32; ks += KW) {
       const int rA = ks * 32 + 8 * g + q, rB = rA + 4;   // tile pixels of this lane's rows
       bf16x8_t A[MO];
@@ -704,73 +774,132 @@ __global__ __launch_bounds__(256) void wgrad_bf16_kernel(WgBParams p) {
       }
     }
   }
-  if (do_db && o0 + tid < p.cout) atomicAdd(p.db + o0 + tid, bsum * p.scale);
-  if (KW > 1) {
+
+  float* red = reinterpret_cast<float*>(smem);
+  // ---- bias gradient: thread tid holds channel group v = tid % GV (256 % GV == 0)
+  if (do_db) {
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);   // [KW][wmn][MO][NC][9][64][4]
-    constexpr int PER = MO * NC * 9 * 64 * 4;
-    float* mine = red + ((size_t)wk * (4 / KW) + wmn) * PER;
-    if (wk > 0) {
 #pragma unroll
-      for (int a = 0; a < MO; ++a)
-#pragma unroll
-        for (int b = 0; b < NC; ++b)
-#pragma unroll
-          for (int t = 0; t < 9; ++t)
-            *reinterpret_cast<f32x4_t*>(mine + (((a * NC + b) * 9 + t) * 64 + lane) * 4) = acc[a][b][t];
-    }
+    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = bs[e];
     __syncthreads();
-    if (wk != 0) return;
-    for (int k = 1; k < KW; ++k) {
-      const float* other = red + ((size_t)k * (4 / KW) + wmn) * PER;
-#pragma unroll
-      for (int a = 0; a < MO; ++a)
-#pragma unroll
-        for (int b = 0; b < NC; ++b)
-#pragma unroll
-          for (int t = 0; t < 9; ++t)
-            acc[a][b][t] += *reinterpret_cast<const f32x4_t*>(other + (((a * NC + b) * 9 + t) * 64 + lane) * 4);
+    if (tid < BO && o0 + tid < p.cout) {
+      const int v = tid >> 3, e = tid & 7;
+      float s = 0.f;
+      for (int r = v; r < 256; r += GV) s += red[r * 8 + e];
+      const int o = o0 + tid;
+      if (p.mode == WG_SLABS)
+        p.ws[blockIdx.z * p.slab + (size_t)p.cout * p.cin * 9 + o] = s;
+      else if (p.mode == WG_DIRECT)
+        p.db[o] += s * p.scale;
+      else
+        atomicAdd(p.db + o, s * p.scale);
     }
   }
-  // acc[mo][nc][tap][j]: o = o0 + (wo*MO+mo)*16 + 4g + j, c = c0 + (wc*NC+nc)*16 + i16.
-  // Transpose each (mo, nc, j) slice through a per-wave LDS scratch so that every atomic
-  // wave-instruction covers contiguous [c][tap] runs of one OIHW row (full atomic rate;
-  // lanes 36 B apart would hit ~36 lines per instruction).
-  if (KW == 1) __syncthreads();
-  float* scr = reinterpret_cast<float*>(smem) +
-               (KW > 1 ? (size_t)wmn * (MO * NC * 9 * 64 * 4) : (size_t)wid * 576);
+  // ---- epilogue, one (mo, nc) 16x16x9 block per round: every wave dumps its partial
+  // accumulators to LDS ([wave][tap][lane][j]); all 256 threads then sum the KW
+  // partials of each (o, c, tap) and write [o][c][tap] runs contiguously.
+  float* slab = p.mode == WG_SLABS ? p.ws + blockIdx.z * p.slab : nullptr;
+#pragma unroll 1
+  for (int r = 0; r < MO * NC; ++r) {
+    const int a = r / NC, b = r % NC;
+    __syncthreads();
+    float* mine = red + (size_t)wid * (9 * 64 * 4);
 #pragma unroll
-  for (int mo = 0; mo < MO; ++mo)
+    for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
-    for (int nc = 0; nc < NC; ++nc)
+      for (int nc = 0; nc < NC; ++nc)
+        if (mo == a && nc == b) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) scr[(g * 16 + i16) * 9 + tap] = acc[mo][nc][tap][j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int it = 0; it < 9; ++it) {
-          const int idx = it * 64 + lane;
-          const int gg = idx / 144, rem = idx - gg * 144;
-          const int c = c0 + (wc * NC + nc) * 16 + rem / 9, tap = rem % 9;
-          const int o = o0 + (wo * MO + mo) * 16 + 4 * gg + j;
-          if (o < p.cout && c < p.cin)
-            atomicAdd(p.dw + ((size_t)o * p.cin + c) * 9 + tap, scr[idx] * p.scale);
+          for (int t = 0; t < 9; ++t)
+            *reinterpret_cast<f32x4_t*>(mine + (t * 64 + lane) * 4) = acc[mo][nc][t];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    constexpr int NOUT = (4 / KW) * 2304;   // outputs of this round (per wmn: 16 o x 16 c x 9)
+    for (int e = tid; e < NOUT; e += 256) {
+      const int m = e / 2304, rem = e - m * 2304;
+      const int ol = rem / 144, rem2 = rem - ol * 144;
+      const int cl = rem2 / 9, tap = rem2 - cl * 9;
+      const int src = ((tap * 64 + (ol >> 2) * 16 + cl) * 4) + (ol & 3);
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < KW; ++k) v += red[(size_t)(m * KW + k) * (9 * 64 * 4) + src];
+      const int mwo = m / WNC, mwc = m % WNC;
+      const int o = o0 + (mwo * MO + a) * 16 + ol;
+      const int c = c0 + (mwc * NC + b) * 16 + cl;
+      if (o < p.cout && c < p.cin) {
+        const size_t off = ((size_t)o * p.cin + c) * 9 + tap;
+        if (p.mode == WG_SLABS)
+          slab[off] = v;
+        else if (p.mode == WG_DIRECT)
+          p.dw[off] += v * p.scale;
+        else
+          atomicAdd(p.dw + off, v * p.scale);
       }
+    }
+  }
+}
+
+// Sum the split slabs: block (x, y) adds slabs [y*spb, (y+1)*spb) of 256 consecutive
+// outputs; one atomic per output per y (plain read-modify-write when gridDim.y == 1).
+__global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t slab, int splits,
+                                                         int spb, int nw, float* dw, float* db,
+                                                         float scale) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= slab) return;
+  const int s0 = blockIdx.y * spb, s1 = min(splits, s0 + spb);
+  float s = 0.f;
+  for (int k = s0; k < s1; ++k) s += ws[(size_t)k * slab + i];
+  float* dst = i < (size_t)nw ? dw + i : (db ? db + (i - nw) : nullptr);
+  if (!dst) return;
+  if (gridDim.y == 1)
+    *dst += s * scale;
+  else
+    atomicAdd(dst, s * scale);
+}
+
+struct WgbPlan {
+  int MO, NC, WMO, WNC;
+  int ot, ct, splits, tiles_per_split, ntiles;
+  TileCfg tc;
+  size_t slab;
+};
+
+WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
+  WgbPlan pl;
+  const int co = d->cout, ci = d->cin;
+  pl.MO = co <= 16 ? 1 : co <= 32 ? 2 : 4;
+  pl.NC = 1;
+  pl.WMO = 1;
+  pl.WNC = ci <= 16 ? 1 : ci <= 32 ? 2 : 1;
+  const int BO = pl.WMO * pl.MO * 16, BC = pl.WNC * pl.NC * 16;
+  pl.tc = pick_tile(d->H, d->W, WGB_BP, 32);
+  pl.ntiles = pg_cdiv(d->B, pl.tc.NB) * (d->W / pl.tc.TW) * (d->H / pl.tc.TH);
+  pl.ot = pg_cdiv(co, BO);
+  pl.ct = pg_cdiv(ci, BC);
+  const int base = pl.ot * pl.ct;
+  // >= 256 workgroups without a split when the output tiles allow it; otherwise split
+  // the pixels up to ~1024 workgroups, keeping >= 2 tiles per split
+  int splits = base >= 256 ? 1 : pg_cdiv(1024, base);
+  const int max_splits = pl.ntiles / 2 > 1 ? pl.ntiles / 2 : 1;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  pl.tiles_per_split = pg_cdiv(pl.ntiles, splits);
+  pl.splits = pg_cdiv(pl.ntiles, pl.tiles_per_split);
+  pl.slab = (size_t)co * ci * 9 + co;
+  return pl;
+}
+
+size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
+  WgbPlan pl = wgrad_bf16_plan(d);
+  return pl.splits > 1 ? pl.splits * pl.slab * sizeof(float) : 0;
 }
 
 template <int MO, int NC, int WMO, int WNC>
-int launch_wgrad_bf16(const pg_conv_desc* d, const void* x, const void* gz, float scale, float* dw,
-                      float* db, hipStream_t st) {
+int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
+                      float scale, float* dw, float* db, float* ws, size_t ws_bytes,
+                      hipStream_t st) {
   constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
-  TileCfg tc = pick_tile(d->H, d->W, WGB_BP, 32);
   WgBParams p;
   p.x = (const bf16_t*)x; p.gz = (const bf16_t*)gz; p.dw = dw; p.db = db;
   p.B = d->B; p.H = d->H; p.W = d->W;
@@ -779,24 +908,28 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const void* x, const void* gz, floa
   p.Win = p.ups ? d->W / 2 : d->W;
   p.cin = d->cin; p.cout = d->cout; p.x_cs = d->x_cs; p.gz_cs = d->y_cs;
   p.scale = scale;
-  p.NB = tc.NB; p.TH = tc.TH; p.TW = tc.TW;
-  p.tiles_x = d->W / tc.TW;
-  p.tiles_y = d->H / tc.TH;
-  p.ntiles = pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y;
+  p.NB = pl.tc.NB; p.TH = pl.tc.TH; p.TW = pl.tc.TW;
+  p.tiles_x = d->W / pl.tc.TW;
+  p.tiles_y = d->H / pl.tc.TH;
+  p.ntiles = pl.ntiles;
+  p.tiles_per_split = pl.tiles_per_split;
   p.GZS = BO + 8;
   p.HS = BC + 8;
-  p.halo_elems = tc.NB * (tc.TH + 2) * (tc.TW + 2);
-  const int ot = pg_cdiv(d->cout, BO), ct = pg_cdiv(d->cin, BC);
-  // >= 4 pixel tiles per workgroup keeps the atomic bytes per MFMA flop low
-  int splits = pg_cdiv(512, ot * ct);
-  const int max_splits = p.ntiles / 4 > 1 ? p.ntiles / 4 : 1;
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  p.tiles_per_split = pg_cdiv(p.ntiles, splits);
-  splits = pg_cdiv(p.ntiles, p.tiles_per_split);
+  p.halo_elems = pl.tc.NB * (pl.tc.TH + 2) * (pl.tc.TW + 2);
+  PG_CHECK_ARG(p.halo_elems <= WGB_MAXHALO, "wgrad_bf16: halo %d > %d", p.halo_elems, WGB_MAXHALO);
+  p.slab = pl.slab;
+  p.ws = nullptr;
+  if (pl.splits == 1) {
+    p.mode = WG_DIRECT;
+  } else if (ws && ws_bytes >= pl.splits * pl.slab * sizeof(float)) {
+    p.mode = WG_SLABS;
+    p.ws = ws;
+  } else {
+    p.mode = WG_ATOMIC;
+  }
   int lds = (WGB_BP * p.GZS + p.halo_elems * p.HS) * 2;
-  const int red = KW > 1 ? 4 * MO * NC * 9 * 64 * 4 * 4 : 0;
-  if (red > lds) lds = red;
+  const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
+  if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
   static bool attr_done = false;
   if (!attr_done) {
@@ -804,22 +937,39 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const void* x, const void* gz, floa
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC>), dim3(ot, ct, splits), dim3(256), lds,
-                     st, p);
+  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC>), dim3(pl.ot, pl.ct, pl.splits),
+                     dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
+  if (p.mode == WG_SLABS) {
+    const int nblk = (int)pg_cdiv((long long)pl.slab, 256);
+    int ry = pg_cdiv(512, nblk);
+    if (ry > pl.splits) ry = pl.splits;
+    const int spb = pg_cdiv(pl.splits, ry);
+    ry = pg_cdiv(pl.splits, spb);
+    hipLaunchKernelGGL(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, (const float*)ws,
+                       pl.slab, pl.splits, spb, d->cout * d->cin * 9, dw, db, scale);
+    PG_LAUNCH_CHECK();
+  }
   return PG_OK;
 }
 
 int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                        float* dw, float* db, hipStream_t st) {
+                        float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st) {
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
-  const int co = d->cout, ci = d->cin;
-  if (co <= 16 && ci <= 16) return launch_wgrad_bf16<1, 1, 1, 1>(d, x, gz, scale, dw, db, st);
-  if (co <= 16 && ci <= 32) return launch_wgrad_bf16<1, 2, 1, 1>(d, x, gz, scale, dw, db, st);
-  if (co <= 32 && ci <= 16) return launch_wgrad_bf16<2, 1, 1, 1>(d, x, gz, scale, dw, db, st);
-  if (co >= 64 && ci >= 64) return launch_wgrad_bf16<2, 2, 2, 2>(d, x, gz, scale, dw, db, st);
-  return launch_wgrad_bf16<1, 1, 2, 2>(d, x, gz, scale, dw, db, st);
+  const WgbPlan pl = wgrad_bf16_plan(d);
+#define PG_WGB(a, b, c, e)                                                                \
+  if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e)                             \
+    return launch_wgrad_bf16<a, b, c, e>(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
+  PG_WGB(1, 1, 1, 1)
+  PG_WGB(1, 1, 1, 2)
+  PG_WGB(2, 1, 1, 1)
+  PG_WGB(2, 1, 1, 2)
+  PG_WGB(4, 1, 1, 1)
+  PG_WGB(4, 1, 1, 2)
+#undef PG_WGB
+  PG_CHECK_ARG(false, "wgrad_bf16: no kernel for plan");
+  return PG_ERR_ARG;
 }
 
 // --------------------------------------------------------------------------
@@ -1064,11 +1214,16 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
   return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
 }
 
+size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d) {
+  return (d && dtype == PG_BF16) ? wgrad_bf16_ws_bytes(d) : 0;
+}
+
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, float* db, void* stream) {
+                     float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
-  if (dtype == PG_BF16) return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (hipStream_t)stream);
+  if (dtype == PG_BF16)
+    return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream);
   TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
   WgParams p;
   p.x = x; p.gz = gz; p.dw = dw; p.db = db;

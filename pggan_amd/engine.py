@@ -167,6 +167,7 @@ class StepEngine:
         self.mcs = cinp(d[0] + 1)
         self.keep_fake_D = False
         self.ws = None          # split-K workspace (fp32), grown on first use
+        self._ws_cache = {}
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -296,18 +297,33 @@ class StepEngine:
         pf, pd, bs, _ = self.packs[(net, key)]
         if not dgrad and bias:
             flags |= L.CONV_BIAS
-        need = self.ops.conv_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout)
-        if need and (self.ws is None or self.ws.numel() * 4 < need):
-            self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
+        need = self._ws_need("c", H, cin, cout, False)
         self.ops.conv3x3(x, pd if dgrad else pf, y, B=self.B, H=H, W=H, cin=cin, cout=cout,
                          flags=flags, slope=SLOPE, out_scale=out_scale,
                          bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2,
                          ws=self.ws if need else None)
 
+    def _ws_need(self, kind, H, cin, cout, ups):
+        """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape); the
+        shared workspace grows to the largest need (launches are stream-ordered)."""
+        key = (kind, H, cin, cout, ups)
+        need = self._ws_cache.get(key)
+        if need is None:
+            if kind == "c":
+                need = self.ops.conv_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout)
+            else:
+                need = self.ops.wgrad_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout,
+                                                      ups=ups)
+            self._ws_cache[key] = need
+        if need and (self.ws is None or self.ws.numel() * 4 < need):
+            self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
+        return need
+
     def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None):
         c = self.packs[(net, key)][3]
+        need = self._ws_need("w", H, cin, cout, ups)
         self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c,
-                            db=db)
+                            db=db, ws=self.ws if need else None)
 
     # ================================================================== G
     def g_forward(self, P, z, alpha):

@@ -102,7 +102,10 @@ class CpuOps:
         else:
             y[..., :cout] = z
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None):
+    def wgrad_workspace_bytes(self, *, B, H, W, cin, cout, ups=False):
+        return 0
+
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None):
         xin = nchw(x, cin)
         if ups:
             xin = up2(xin)

@@ -121,11 +121,22 @@ def test_conv3x3_dgrad_pack(case, dtype):
     cmp(outs[0], outs[1], tol_for(dtype), "dgrad")
 
 
+WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, False),
+               (1, 64, 8, 8, False), (2, 32, 64, 32, True),
+               # bench-like: many pixel splits (slabs), direct single split, ups + cin 32
+               (4, 128, 16, 32, False), (4, 32, 512, 512, False), (2, 64, 32, 16, True),
+               (4, 64, 64, 128, False)]
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, False),
-                                  (1, 64, 8, 8, False), (2, 32, 64, 32, True)])
-def test_conv3x3_wgrad(case, dtype):
+@pytest.mark.parametrize("use_ws", [True, False])
+@pytest.mark.parametrize("case", WGRAD_CASES)
+def test_conv3x3_wgrad(case, dtype, use_ws):
+    """Weight + fused bias gradient; with a workspace the split partials go through slabs
+    and the reduction kernel, without one through atomics."""
     B, H, cin, cout, ups = case
+    if dtype == torch.float32 and not use_ws:
+        pytest.skip("the f32 kernel takes no workspace")
     hip, cpu = ops_pair(dtype)
     Hin = H // 2 if ups else H
     x = q(rnd(B, Hin, Hin, cinp(cin), seed=11), dtype)
@@ -134,10 +145,17 @@ def test_conv3x3_wgrad(case, dtype):
     for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
         dt = dtype if dev == "cuda" else torch.float32
         dw = torch.full((cout, cin, 3, 3), 0.5, device=dev)
+        db = torch.full((cout,), 0.25, device=dev)
+        ws = None
+        if use_ws and dev == "cuda":
+            nb = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=ups)
+            ws = torch.full((max(nb // 4, 1),), float("nan"), device=dev)
         ops.conv_wgrad(x.to(dev).to(dt), gz.to(dev).to(dt), dw, B=B, H=H, W=H, cin=cin, cout=cout,
-                       ups=ups, scale=0.3)
-        outs.append(dw)
-    cmp(outs[0], outs[1], 2e-5 if dtype == torch.float32 else 1e-4, "wgrad")
+                       ups=ups, scale=0.3, db=db, ws=ws)
+        outs.append((dw, db))
+    tol = 2e-5 if dtype == torch.float32 else 1e-4
+    cmp(outs[0][0], outs[1][0], tol, "wgrad")
+    cmp(outs[0][1], outs[1][1], tol, "wgrad bias")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

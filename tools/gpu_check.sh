@@ -43,6 +43,11 @@ for step in "$@"; do
         --write gpurun_out/pmc_WRITE_SIZE \
         -o gpurun_out/prof_summary.json > /dev/null ;;
     shapes) PG_BENCH_SHAPES=gpurun_out/shapes.json run shapes 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
+    wg) run wg 600 python -m pytest tests/test_gpu_ops.py -q -x -k wgrad ;;
+    kbw) run kbw 300 python tools/kbench.py w:1024:16:32:0 w:1024:16:16:0 w:1024:32:16:1 \
+           w:512:32:64:0 w:512:32:32:0 w:256:64:128:0 w:256:64:64:0 w:128:128:256:0 \
+           w:128:128:128:0 w:64:256:512:0 w:64:256:256:0 w:32:512:512:0 w:16:512:512:0 \
+           w:8:512:512:0 w:4:512:512:0 w:4:513:512:0 ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
