@@ -255,6 +255,14 @@ def main():
     dt = time.perf_counter() - t0
     if timer:
         timer.on = False
+    # host-side cost of enqueueing one step (kernels are not waited for): if this is close
+    # to ms_per_step the step is launch-bound, not GPU-bound
+    torch.cuda.synchronize()
+    h0 = time.perf_counter()
+    for _ in range(2):
+        step()
+    host_ms = (time.perf_counter() - h0) * 1e3 / 2
+    torch.cuda.synchronize()
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -310,6 +318,7 @@ def main():
                                    f"alpha {args.alpha}, depths {depths}",
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
+            "host_enqueue_ms_per_step": round(host_ms, 3),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -815,26 +815,41 @@ void wgrad_bf16_kernel(WgBParams p) {
         }
     __syncthreads();
     constexpr int NOUT = (4 / KW) * 2304;   // outputs of this round (per wmn: 16 o x 16 c x 9)
-    for (int e = tid; e < NOUT; e += 256) {
+    constexpr int NPT = NOUT / 256;
+    float v[NPT];
+    int offs[NPT];
+#pragma unroll
+    for (int k2 = 0; k2 < NPT; ++k2) {
+      const int e = tid + 256 * k2;
       const int m = e / 2304, rem = e - m * 2304;
       const int ol = rem / 144, rem2 = rem - ol * 144;
       const int cl = rem2 / 9, tap = rem2 - cl * 9;
       const int src = ((tap * 64 + (ol >> 2) * 16 + cl) * 4) + (ol & 3);
-      float v = 0.f;
+      float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < KW; ++k) v += red[(size_t)(m * KW + k) * (9 * 64 * 4) + src];
+      for (int k = 0; k < KW; ++k) sum += red[(size_t)(m * KW + k) * (9 * 64 * 4) + src];
       const int mwo = m / WNC, mwc = m % WNC;
       const int o = o0 + (mwo * MO + a) * 16 + ol;
       const int c = c0 + (mwc * NC + b) * 16 + cl;
-      if (o < p.cout && c < p.cin) {
-        const size_t off = ((size_t)o * p.cin + c) * 9 + tap;
-        if (p.mode == WG_SLABS)
-          slab[off] = v;
-        else if (p.mode == WG_DIRECT)
-          p.dw[off] += v * p.scale;
-        else
-          atomicAdd(p.dw + off, v * p.scale);
-      }
+      v[k2] = sum;
+      offs[k2] = (o < p.cout && c < p.cin) ? (o * p.cin + c) * 9 + tap : -1;
+    }
+    if (p.mode == WG_DIRECT) {
+      // all loads first, then all stores (one DRAM round trip instead of NPT)
+      float old[NPT];
+#pragma unroll
+      for (int k2 = 0; k2 < NPT; ++k2) old[k2] = offs[k2] >= 0 ? p.dw[offs[k2]] : 0.f;
+#pragma unroll
+      for (int k2 = 0; k2 < NPT; ++k2)
+        if (offs[k2] >= 0) p.dw[offs[k2]] = old[k2] + v[k2] * p.scale;
+    } else if (p.mode == WG_SLABS) {
+#pragma unroll
+      for (int k2 = 0; k2 < NPT; ++k2)
+        if (offs[k2] >= 0) slab[offs[k2]] = v[k2];
+    } else {
+#pragma unroll
+      for (int k2 = 0; k2 < NPT; ++k2)
+        if (offs[k2] >= 0) atomicAdd(p.dw + offs[k2], v[k2] * p.scale);
     }
   }
 }
@@ -898,7 +913,6 @@ template <int MO, int NC, int WMO, int WNC>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
                       float scale, float* dw, float* db, float* ws, size_t ws_bytes,
                       hipStream_t st) {
-  constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
   WgBParams p;
   p.x = (const bf16_t*)x; p.gz = (const bf16_t*)gz; p.dw = dw; p.db = db;
@@ -1138,9 +1152,14 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
   return launch_conv<T, BM, BN, 4, 1, 12, true>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
 }
 
+#include "conv_hr.inc"
+
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                   const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, st);
+  }
   int BM, BN;
   conv_tile_for(d->cout, &BM, &BN, d->W);
   // cout >= 64: [pixel][cout] MFMA + LDS-transposed epilogue; cout <= 32: [cout][pixel]

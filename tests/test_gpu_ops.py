@@ -59,6 +59,18 @@ CONV_CASES = [
     (1, 64, 16, 32, ("pool", "accum")),
     (4, 4, 33, 32, ("bias", "lrelu")),          # mbstd-style padded cin (33 -> 64)
     (2, 8, 32, 20, ("bias",)),                  # cout not a multiple of 16
+    # H, W >= 16: the compile-time-geometry kernel (conv_hr.inc), persistent when cin <= 32
+    (2, 32, 16, 16, ("bias", "lrelu")),
+    (2, 32, 16, 32, ("ups", "bias", "lrelu")),
+    (2, 32, 32, 16, ("mask",)),
+    (2, 32, 16, 32, ("bias", "lrelu", "pool")),
+    (1, 64, 32, 64, ("bias", "lrelu", "pool")),
+    (2, 64, 64, 32, ("mask", "accum")),
+    (1, 32, 128, 64, ("bias", "lrelu")),
+    (2, 16, 16, 16, ("mask", "accum")),
+    (4, 512, 16, 16, ("bias", "lrelu")),        # > 2048 tiles: several tiles per workgroup
+    (4, 512, 32, 16, ("mask",)),
+    (4, 512, 16, 32, ("ups", "bias", "lrelu", "pool")),
 ]
 
 

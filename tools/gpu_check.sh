@@ -48,6 +48,11 @@ for step in "$@"; do
            w:512:32:64:0 w:512:32:32:0 w:256:64:128:0 w:256:64:64:0 w:128:128:256:0 \
            w:128:128:128:0 w:64:256:512:0 w:64:256:256:0 w:32:512:512:0 w:16:512:512:0 \
            w:8:512:512:0 w:4:512:512:0 w:4:513:512:0 ;;
+    conv) run conv 600 python -m pytest tests/test_gpu_ops.py -q -x -k "conv3x3_fwd or dgrad" ;;
+    kbc) run kbc 300 python tools/kbench.py c:1024:32:16:8 c:1024:16:16:8 c:1024:16:32:22 \
+           c:1024:16:16:6 c:512:64:32:8 c:512:32:64:22 c:512:32:32:6 c:512:32:32:0 \
+           c:256:128:64:8 c:256:64:128:22 c:256:64:64:6 c:128:256:128:8 c:128:128:128:6 \
+           c:64:512:256:8 c:64:256:256:6 c:32:512:512:8 c:1024:32:16:7 c:1024:16:32:8 ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
