@@ -17,6 +17,7 @@
 // Reference: lib/layers.py:58-89 (conv*c incl. bias), lib/blocks.py:113-201.
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -637,8 +638,8 @@ constexpr int WGB_MAXHALO = 288;   // max halo pixels of a 128-pixel tile (pick_
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <int MO, int NC, int WMO, int WNC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MO >= 4 ? 2 : MO == 2 ? 3 : 4)))
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void wgrad_bf16_kernel(WgBParams p) {
   constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
@@ -693,8 +694,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       if (c0 + 8 * v < p.x_cs) hpk[k] = (nb << 24) | (hy << 16) | (hx << 8) | v;
     }
   }
-  u32x4_t rg[NGZ], rh[NH];
-  auto load_tile = [&](int t) {
+  auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH]) {
     const int tx0 = (t % p.tiles_x) * p.TW;
     int tt = t / p.tiles_x;
     const int ty0 = (tt % p.tiles_y) * p.TH;
@@ -718,12 +718,7 @@ void wgrad_bf16_kernel(WgBParams p) {
             xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff));
     }
   };
-
-  const int t_begin = blockIdx.z * p.tiles_per_split;
-  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
-  if (t_begin < t_end) load_tile(t_begin);
-  for (int t = t_begin; t < t_end; ++t) {
-    __syncthreads();   // the previous tile's fragments have been read
+  auto store_tile = [&](const u32x4_t (&rg)[NGZ], const u32x4_t (&rh)[NH]) {
 #pragma unroll
     for (int k = 0; k < NGZ; ++k) {
       const int i = tid + k * 256;
@@ -745,9 +740,23 @@ void wgrad_bf16_kernel(WgBParams p) {
         *reinterpret_cast<u32x4_t*>(hal + hp * p.HS + 8 * v) = rh[k];
       }
     }
-    __syncthreads();
-    if (t + 1 < t_end) load_tile(t + 1);   // in flight during this tile's MFMAs
-    for (int ks = wk; ks < WGB_BP / 32; ks += KW) {
+  };
+  // halo rows of this lane's two k-rows for each k-step the wave owns (tile-invariant)
+  constexpr int KSW = (WGB_BP / 32) / KW;
+  int hAo[KSW], hBo[KSW];
+#pragma unroll
+  for (int j = 0; j < KSW; ++j) {
+    const int ks = wk + j * KW;
+    const int rA = ks * 32 + 8 * g + q, rB = rA + 4;
+    const int txA = rA % p.TW, tyA = (rA / p.TW) % p.TH, nbA = rA / (p.TW * p.TH);
+    const int txB = rB % p.TW, tyB = (rB / p.TW) % p.TH, nbB = rB / (p.TW * p.TH);
+    hAo[j] = (nbA * (p.TH + 2) + tyA) * TW2 + txA;
+    hBo[j] = (nbB * (p.TH + 2) + tyB) * TW2 + txB;
+  }
+  auto compute_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < KSW; ++j) {
+      const int ks = wk + j * KW;
       const int rA = ks * 32 + 8 * g + q, rB = rA + 4;   // tile pixels of this lane's rows
       bf16x8_t A[MO];
 #pragma unroll
@@ -755,10 +764,7 @@ void wgrad_bf16_kernel(WgBParams p) {
         const int ol = (wo * MO + mo) * 16 + 4 * pq;
         A[mo] = tr_read8(gzl + rA * p.GZS + ol, gzl + rB * p.GZS + ol);
       }
-      const int txA = rA % p.TW, tyA = (rA / p.TW) % p.TH, nbA = rA / (p.TW * p.TH);
-      const int txB = rB % p.TW, tyB = (rB / p.TW) % p.TH, nbB = rB / (p.TW * p.TH);
-      const int hA = (nbA * (p.TH + 2) + tyA) * TW2 + txA;
-      const int hB = (nbB * (p.TH + 2) + tyB) * TW2 + txB;
+      const int hA = hAo[j], hB = hBo[j];
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int toff = (tap / 3) * TW2 + (tap % 3);
@@ -771,6 +777,27 @@ void wgrad_bf16_kernel(WgBParams p) {
             acc[mo][nc][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mo], Bf, acc[mo][nc][tap],
                                                                        0, 0, 0);
         }
+      }
+    }
+  };
+
+  // PD tiles of global loads in flight: tile t+PD is fetched into the register set that
+  // tile t just left, right after it was written to LDS
+  u32x4_t rg[PD][NGZ], rh[PD][NH];
+  const int t_begin = blockIdx.z * p.tiles_per_split;
+  const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    if (t_begin + d < t_end) load_tile(t_begin + d, rg[d], rh[d]);
+  for (int t = t_begin; t < t_end; t += PD) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      if (t + d < t_end) {
+        __syncthreads();   // the previous tile's fragments have been read
+        store_tile(rg[d], rh[d]);
+        __syncthreads();
+        if (t + d + PD < t_end) load_tile(t + d + PD, rg[d], rh[d]);
+        compute_tile();
       }
     }
   }
@@ -894,7 +921,11 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   const int base = pl.ot * pl.ct;
   // >= 256 workgroups without a split when the output tiles allow it; otherwise split
   // the pixels up to ~1024 workgroups, keeping >= 2 tiles per split
-  int splits = base >= 256 ? 1 : pg_cdiv(1024, base);
+  // wide (MO = 4) tiles run one workgroup per CU with 4 tiles of loads in flight: one
+  // wave of workgroups; the HBM-bound narrow ones use ~4 per CU
+  int target = pl.MO >= 4 ? 256 : 1024;
+  if (const char* e = getenv("PG_WG_TARGET")) target = atoi(e);   // tuning runs only
+  int splits = base >= 256 ? 1 : pg_cdiv(target, base);
   const int max_splits = pl.ntiles / 2 > 1 ? pl.ntiles / 2 : 1;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -909,7 +940,7 @@ size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
   return pl.splits > 1 ? pl.splits * pl.slab * sizeof(float) : 0;
 }
 
-template <int MO, int NC, int WMO, int WNC>
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
                       float scale, float* dw, float* db, float* ws, size_t ws_bytes,
                       hipStream_t st) {
@@ -947,11 +978,11 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC>,
+    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC>), dim3(pl.ot, pl.ct, pl.splits),
+  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   if (p.mode == WG_SLABS) {
@@ -972,15 +1003,24 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
   const WgbPlan pl = wgrad_bf16_plan(d);
-#define PG_WGB(a, b, c, e)                                                                \
-  if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e)                             \
-    return launch_wgrad_bf16<a, b, c, e>(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
-  PG_WGB(1, 1, 1, 1)
-  PG_WGB(1, 1, 1, 2)
-  PG_WGB(2, 1, 1, 1)
-  PG_WGB(2, 1, 1, 2)
-  PG_WGB(4, 1, 1, 1)
-  PG_WGB(4, 1, 1, 2)
+  // (prefetch depth, waves per SIMD); PG_WG_VARIANT="pd,wpe" overrides for tuning runs
+  int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
+  if (const char* e = getenv("PG_WG_VARIANT")) sscanf(e, "%d,%d", &pd, &wpe);
+#define PG_WGB(a, b, c, e, PD, WPE)                                                      \
+  if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e && pd == PD && wpe == WPE)  \
+    return launch_wgrad_bf16<a, b, c, e, PD, WPE>(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
+  PG_WGB(1, 1, 1, 1, 2, 3)
+  PG_WGB(1, 1, 1, 2, 2, 2)
+  PG_WGB(2, 1, 1, 1, 2, 2)
+  PG_WGB(2, 1, 1, 2, 2, 2)
+  PG_WGB(4, 1, 1, 1, 1, 2)
+  PG_WGB(4, 1, 1, 1, 2, 2)
+  PG_WGB(4, 1, 1, 1, 2, 1)
+  PG_WGB(4, 1, 1, 1, 4, 1)
+  PG_WGB(4, 1, 1, 2, 1, 2)
+  PG_WGB(4, 1, 1, 2, 2, 2)
+  PG_WGB(4, 1, 1, 2, 2, 1)
+  PG_WGB(4, 1, 1, 2, 4, 1)
 #undef PG_WGB
   PG_CHECK_ARG(false, "wgrad_bf16: no kernel for plan");
   return PG_ERR_ARG;

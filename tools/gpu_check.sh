@@ -53,6 +53,19 @@ for step in "$@"; do
            c:1024:16:16:6 c:512:64:32:8 c:512:32:64:22 c:512:32:32:6 c:512:32:32:0 \
            c:256:128:64:8 c:256:64:128:22 c:256:64:64:6 c:128:256:128:8 c:128:128:128:6 \
            c:64:512:256:8 c:64:256:256:6 c:32:512:512:8 c:1024:32:16:7 c:1024:16:32:8 ;;
+    wgsweep)
+      S="w:512:32:64:0 w:256:64:128:0 w:256:64:64:0 w:128:128:256:0 w:128:128:128:0 w:64:256:512:0 w:64:256:256:0 w:32:512:512:0 w:16:512:512:0"
+      for v in 1,2 2,1 4,1; do for tg in 256 512 1024; do
+        echo "== variant $v target $tg" >> gpurun_out/wgsweep.log
+        PG_WG_VARIANT=$v PG_WG_TARGET=$tg timeout -k 10 120 python tools/kbench.py $S >> gpurun_out/wgsweep.log 2>&1 || exit 1
+      done; done; echo "wgsweep done" ;;
+    pmcq)   # counters of one kbench spec: PMC_SPEC, PMC_COUNTERS (one pass)
+      ROOT=$(pwd); export TMPDIR=/tmp
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --pmc ${PMC_COUNTERS} --output-format csv \
+          -d "$ROOT/gpurun_out/pmcq" -o run -- python "$ROOT/tools/kbench.py" --iters 3 ${PMC_SPEC} ) \
+          > gpurun_out/pmcq.log 2>&1
+      rc=$?; echo "pmcq rc=$rc"; tail -n 3 gpurun_out/pmcq.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    listc) ( rocprofv3 -L > gpurun_out/counters.txt 2>&1 ); echo "listc rc=$?" ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
