@@ -66,6 +66,22 @@ typedef struct {
 size_t pg_conv3x3_packed_elems(int mode, int cout, int cin);
 int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw, float scale,
                     void* wpk, void* stream);
+/* All conv weights of a net in one launch: for each item, fwd and dgrad packs (as
+ * pg_conv3x3_pack) and bias_scaled[o] = scale * bias[o] (bias may be NULL).  `items` is a
+ * DEVICE array of n pg_pack_item (built once; the pointers are stable across steps);
+ * max_tiles = max over items of ceil(max(cout16, cinp(cout))/32) * ceil(max(cinp(cin), cin16)/32). */
+typedef struct {
+  const float* w;       /* [cout][cin][3][3] fp32 */
+  const float* bias;    /* [cout] or NULL */
+  void* fwd;            /* PG_PACK_FWD layout, dtype */
+  void* dgrad;          /* PG_PACK_DGRAD layout, dtype */
+  float* bias_scaled;   /* [cout] */
+  float scale;
+  int cout, cin;
+  int pad_;
+} pg_pack_item;
+int pg_conv3x3_pack_batch(int dtype, int n, const pg_pack_item* items, int max_tiles,
+                          void* stream);
 /* ws: optional fp32 workspace (>= pg_conv3x3_workspace_size bytes) that enables split-K
  * over input-channel chunks for small-spatial convs (deterministic: partial slabs + a
  * reduction/epilogue kernel); NULL or too small -> single pass. */

@@ -30,6 +30,18 @@ class ConvDesc(ctypes.Structure):
                [("slope", ctypes.c_float), ("out_scale", ctypes.c_float)]
 
 
+class PackItem(ctypes.Structure):
+    """pg_pack_item (include/pggan_hip.h)."""
+    _fields_ = [("w", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("fwd", ctypes.c_void_p),
+                ("dgrad", ctypes.c_void_p), ("bias_scaled", ctypes.c_void_p),
+                ("scale", ctypes.c_float), ("cout", ctypes.c_int), ("cin", ctypes.c_int),
+                ("pad_", ctypes.c_int)]
+
+
+def _cinp(c):
+    return (c + 7) // 8 * 8 if c <= 16 else (c + 31) // 32 * 32
+
+
 class LinearDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("B", "K", "N", "in_cs", "out_cs", "flags")] + \
                [("scale", ctypes.c_float), ("slope", ctypes.c_float)]
@@ -42,6 +54,7 @@ _SIGS = {
     "pg_version": ([], _I),
     "pg_conv3x3_packed_elems": ([_I, _I, _I], _SZ),
     "pg_conv3x3_pack": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_conv3x3_pack_batch": ([_I, _I, _VP, _I, _VP], _I),
     "pg_conv3x3_workspace_size": ([ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
                        _I),
@@ -138,6 +151,29 @@ class HipOps:
         cout, cin = w.shape[0], w.shape[1]
         self._chk(self.lib.pg_conv3x3_pack(self._dt(out), mode, cout, cin, _p(w), scale, _p(out),
                                            self._s()), "conv3x3_pack")
+
+    def pack_table(self, entries):
+        """entries: [(w, bias|None, fwd, dgrad, bias_scaled, scale)] -> (device table, n,
+        max_tiles) for conv_pack_batch.  The table holds raw pointers: rebuild it if any of
+        the tensors is reallocated."""
+        n = len(entries)
+        arr = (PackItem * n)()
+        mt = 1
+        for i, (w, b, pf, pd, bs, sc) in enumerate(entries):
+            self._cuda(w, b, pf, pd, bs)
+            cout, cin = w.shape[0], w.shape[1]
+            arr[i] = PackItem(_p(w), _p(b), _p(pf), _p(pd), _p(bs), float(sc), cout, cin, 0)
+            O = max((cout + 15) // 16 * 16, _cinp(cout))
+            C = max(_cinp(cin), (cin + 15) // 16 * 16)
+            mt = max(mt, ((O + 31) // 32) * ((C + 31) // 32))
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        return raw.to(entries[0][0].device), n, mt
+
+    def conv_pack_batch(self, table):
+        dev, n, mt = table
+        self._cuda(dev)
+        self._chk(self.lib.pg_conv3x3_pack_batch(self.dt, n, _p(dev), mt, self._s()),
+                  "conv3x3_pack_batch")
 
     def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
                 bias=None, aux=None, y2=None, ws=None):

@@ -45,6 +45,7 @@ struct ConvParams {
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
+__device__ __forceinline__ int cinp_of_dev(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
 
 struct TileCfg {
   int BM, BN, NB, TH, TW;
@@ -1048,6 +1049,43 @@ __global__ void pack_kernel(int mode, int cout, int cin, int rows, int kin, cons
   }
 }
 
+// One launch for all conv weights of a net.  Block (x, item): a 32(o) x 32(c) x 9 tile of
+// W staged in LDS (rows read contiguously), then written in the fwd layout (c fastest) and
+// the flipped dgrad layout (o fastest), both coalesced; zero padding included.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_batch_kernel(const pg_pack_item* items) {
+  const pg_pack_item it = items[blockIdx.y];
+  const int cout = it.cout, cin = it.cin;
+  const int rf = (cout + 15) & ~15, kf = cinp_of_dev(cin);   // fwd   [rf][9][kf]
+  const int rd = (cin + 15) & ~15, kd = cinp_of_dev(cout);   // dgrad [rd][9][kd]
+  const int O = rf > kd ? rf : kd, C = kf > rd ? kf : rd;
+  const int tc = (C + 31) / 32;
+  if ((int)blockIdx.x >= ((O + 31) / 32) * tc) return;
+  const int o0 = (blockIdx.x / tc) * 32, c0 = (blockIdx.x % tc) * 32;
+  __shared__ float s[32][32 * 9 + 1];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 32 * 288; i += 256) {
+    const int ol = i / 288, j = i - ol * 288;
+    const int o = o0 + ol, c = c0 + j / 9;
+    s[ol][j] = (o < cout && c < cin) ? it.w[((size_t)o * cin + c0) * 9 + j] * it.scale : 0.f;
+  }
+  __syncthreads();
+  T* fwd = reinterpret_cast<T*>(it.fwd);
+  T* dg = reinterpret_cast<T*>(it.dgrad);
+  for (int i = tid; i < 32 * 288; i += 256) {
+    const int cl = i & 31, tap = (i >> 5) % 9, ol = i / 288;
+    const int o = o0 + ol, c = c0 + cl;
+    if (o < rf && c < kf) Ty<T>::st(fwd + ((size_t)o * 9 + tap) * kf + c, s[ol][cl * 9 + tap]);
+  }
+  for (int i = tid; i < 32 * 288; i += 256) {
+    const int ol = i & 31, tap = (i >> 5) % 9, cl = i / 288;
+    const int o = o0 + ol, c = c0 + cl;
+    if (c < rd && o < kd) Ty<T>::st(dg + ((size_t)c * 9 + tap) * kd + o, s[ol][cl * 9 + 8 - tap]);
+  }
+  if (c0 == 0 && tid < 32 && o0 + tid < cout)
+    it.bias_scaled[o0 + tid] = it.bias ? it.bias[o0 + tid] * it.scale : 0.f;
+}
+
 template <typename T>
 __global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scale, float* db,
                                  int pix_per_block) {
@@ -1242,6 +1280,19 @@ int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw,
   else
     hipLaunchKernelGGL(pack_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
                        kin, w_oihw, scale, (bf16_t*)wpk);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_conv3x3_pack_batch(int dtype, int n, const pg_pack_item* items, int max_tiles,
+                          void* stream) {
+  PG_CHECK_ARG(items && n > 0 && n < 65536 && max_tiles > 0, "conv3x3_pack_batch: bad args");
+  const dim3 grid(max_tiles, n);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == PG_F32)
+    hipLaunchKernelGGL(pack_batch_kernel<float>, grid, dim3(256), 0, st, items);
+  else
+    hipLaunchKernelGGL(pack_batch_kernel<bf16_t>, grid, dim3(256), 0, st, items);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

@@ -280,10 +280,22 @@ class StepEngine:
                     he(cin * 9))
 
     def pack(self, net, P):
-        """Fold the He constant into packed fwd/dgrad weights and scaled biases."""
+        """Fold the He constant into packed fwd/dgrad weights and scaled biases: one batched
+        launch per net (table of pointers built once, rebuilt if a tensor moves)."""
         if not hasattr(self, "packs"):
             self.alloc_packs()
         ops = self.ops
+        if hasattr(ops, "pack_table"):
+            ents = []
+            for key, wname, cout, cin in self._conv_list(net):
+                pf, pd, bs, c = self.packs[(net, key)]
+                ents.append((P[wname + ".weight"], P[wname + ".bias"], pf, pd, bs, c))
+            sig = tuple(t.data_ptr() for e in ents for t in (e[0], e[1]))
+            tabs = self.__dict__.setdefault("_pack_tables", {})
+            if net not in tabs or tabs[net][0] != sig:
+                tabs[net] = (sig, ops.pack_table(ents))
+            ops.conv_pack_batch(tabs[net][1])
+            return
         for key, wname, cout, cin in self._conv_list(net):
             pf, pd, bs, c = self.packs[(net, key)]
             w = P[wname + ".weight"]

@@ -396,3 +396,28 @@ def test_conv3x3_splitk(case, dtype):
     cmp(outs[0][0], outs[1][0], tol_for(dtype), "splitk y")
     if outs[0][1] is not None:
         cmp(outs[0][1], outs[1][1], tol_for(dtype), "splitk y2")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_pack_batch(dtype):
+    """One batched launch == the per-layer fwd / dgrad packs and scaled biases, bit-exact."""
+    hip = lib().HipOps(dtype)
+    shapes = [(16, 16), (32, 16), (16, 32), (64, 32), (512, 513), (20, 33), (512, 512)]
+    ents, refs = [], []
+    for i, (co, ci) in enumerate(shapes):
+        w = rnd(co, ci, 3, 3, seed=40 + i).cuda()
+        b = rnd(co, seed=60 + i).cuda()
+        sc = 0.1 + 0.01 * i
+        pf = torch.full((hip.packed_elems(0, co, ci),), 7.0, device="cuda").to(dtype)
+        pd = torch.full((hip.packed_elems(1, co, ci),), 7.0, device="cuda").to(dtype)
+        bs = torch.zeros(co, device="cuda")
+        ents.append((w, b, pf, pd, bs, sc))
+        rf, rd = torch.zeros_like(pf), torch.zeros_like(pd)
+        hip.conv_pack(0, w, sc, rf)
+        hip.conv_pack(1, w, sc, rd)
+        refs.append((rf, rd, b * sc))
+    hip.conv_pack_batch(hip.pack_table(ents))
+    torch.cuda.synchronize()
+    for (w, b, pf, pd, bs, sc), (rf, rd, rb) in zip(ents, refs):
+        assert torch.equal(pf, rf) and torch.equal(pd, rd)
+        assert torch.allclose(bs, rb, rtol=1e-6, atol=0)

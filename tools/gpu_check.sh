@@ -23,9 +23,10 @@ for step in "$@"; do
     benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
     prof)
       ROOT=$(pwd)
+      rm -rf gpurun_out/prof
       export TMPDIR=/tmp
       ( cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
-          -d "$ROOT/gpurun_out/prof" -o run -- python "$ROOT/bench.py" --steps 3 --warmup 1 \
+          -d "$ROOT/gpurun_out/prof" -o run -- python "$ROOT/bench.py" --steps ${PROF_STEPS:-3} --warmup 1 \
           --cpu-baseline off --no-kernel-events ) > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -n 3 gpurun_out/prof.log
       if [ $rc -ne 0 ]; then exit $rc; fi ;;
