@@ -650,7 +650,12 @@ void wgrad_bf16_kernel(WgBParams p) {
   static_assert(NGZ * 256 == WGB_BP * GV, "gz staging must tile the workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* gzl = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* hal = gzl + WGB_BP * p.GZS;
+  // row r of a tile lives at r*S + (r/8)*64 elements: with S = 16 (mod 32) elements the
+  // transposed fragment reads are bank-conflict free (tools/lds_banks.py)
+  constexpr int GZS = BO + (BO > 16 ? 16 : 0), HS = BC + (BC > 16 ? 16 : 0);
+  auto grow = [](int r) { return r * GZS + (r >> 3) * 64; };
+  auto hrow = [](int r) { return r * HS + (r >> 3) * 64; };
+  bf16_t* hal = gzl + grow(WGB_BP);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid % KW, wmn = wid / KW;
   const int wo = wmn / WNC, wc = wmn % WNC;
@@ -724,7 +729,7 @@ void wgrad_bf16_kernel(WgBParams p) {
     for (int k = 0; k < NGZ; ++k) {
       const int i = tid + k * 256;
       const int pm = i / GV, v = i - pm * GV;
-      *reinterpret_cast<u32x4_t*>(gzl + pm * p.GZS + 8 * v) = rg[k];
+      *reinterpret_cast<u32x4_t*>(gzl + grow(pm) + 8 * v) = rg[k];
       if (do_db) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -738,7 +743,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int i = tid + k * 256;
       if (i < nhalo) {
         const int hp = i / HV, v = i - hp * HV;
-        *reinterpret_cast<u32x4_t*>(hal + hp * p.HS + 8 * v) = rh[k];
+        *reinterpret_cast<u32x4_t*>(hal + hrow(hp) + 8 * v) = rh[k];
       }
     }
   };
@@ -763,7 +768,7 @@ void wgrad_bf16_kernel(WgBParams p) {
 #pragma unroll
       for (int mo = 0; mo < MO; ++mo) {
         const int ol = (wo * MO + mo) * 16 + 4 * pq;
-        A[mo] = tr_read8(gzl + rA * p.GZS + ol, gzl + rB * p.GZS + ol);
+        A[mo] = tr_read8(gzl + grow(rA) + ol, gzl + grow(rB) + ol);
       }
       const int hA = hAo[j], hB = hBo[j];
 #pragma unroll
@@ -772,7 +777,7 @@ void wgrad_bf16_kernel(WgBParams p) {
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
           const int cl = (wc * NC + nc) * 16 + 4 * pq;
-          const bf16x8_t Bf = tr_read8(hal + (hA + toff) * p.HS + cl, hal + (hB + toff) * p.HS + cl);
+          const bf16x8_t Bf = tr_read8(hal + hrow(hA + toff) + cl, hal + hrow(hB + toff) + cl);
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo)
             acc[mo][nc][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mo], Bf, acc[mo][nc][tap],
@@ -959,8 +964,8 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.tiles_y = d->H / pl.tc.TH;
   p.ntiles = pl.ntiles;
   p.tiles_per_split = pl.tiles_per_split;
-  p.GZS = BO + 8;
-  p.HS = BC + 8;
+  p.GZS = BO + (BO > 16 ? 16 : 0);
+  p.HS = BC + (BC > 16 ? 16 : 0);
   p.halo_elems = pl.tc.NB * (pl.tc.TH + 2) * (pl.tc.TW + 2);
   PG_CHECK_ARG(p.halo_elems <= WGB_MAXHALO, "wgrad_bf16: halo %d > %d", p.halo_elems, WGB_MAXHALO);
   p.slab = pl.slab;
@@ -973,7 +978,7 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   } else {
     p.mode = WG_ATOMIC;
   }
-  int lds = (WGB_BP * p.GZS + p.halo_elems * p.HS) * 2;
+  int lds = (WGB_BP * p.GZS + (WGB_BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * 64) * 2;
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
@@ -1167,8 +1172,9 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.KS = (9 * p.CK + 31) / 32;
   p.nchunks = p.cin_p / p.CK;
   const int pb = p.CK * (int)sizeof(T);
-  p.pixb = pb + (pb >= 64 ? 16 : 0);
-  p.wrowb = p.KS * 32 * (int)sizeof(T) + 16;
+  // bf16: paddings that make the b128 fragment reads conflict-free (tools/lds_banks.py)
+  p.pixb = pb + (pb >= 64 ? (sizeof(T) == 2 ? 32 : 16) : 0);
+  p.wrowb = p.KS * 32 * (int)sizeof(T) + (sizeof(T) == 2 ? 32 : 16);
   p.halo_bytes = (tc.NB * (tc.TH + 2) * (tc.TW + 2) * p.pixb + 15) & ~15;
   const int main_bytes = p.halo_bytes + BN * p.wrowb;
   const int epi_bytes = TR ? 0 : BM * (BN + 4) * 4;

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Memory-bound kernels of the PGGAN step: PixelNorm, pooling/unpooling with
 // leaky-relu masks, fade-in blends, to/fromRGB 1x1 layers, equalized linears,
 // minibatch-stddev (fwd / bwd / R1 second order), BCE + R1 / WGAN-GP
@@ -610,6 +611,122 @@ __global__ void linear_fwd_kernel(pg_linear_desc d, const void* x, const float* 
   }
 }
 
+// Linear forward, one workgroup per output feature n.  The K inputs are walked in units
+// of 16 (unit u = input channel c of the CHW flatten k = c*16 + hw, or k = 16u..16u+15):
+// a lane reads the unit's 16 weights as 4 x 16 B and the batch rows' 16 inputs, so both
+// the weight stream and the NHWC activation gather are coalesced across lanes.  The 4
+// waves split the units; partial sums meet in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void linear_fwd_kernel2(pg_linear_desc d, const void* x,
+                                                          const float* w, const float* b,
+                                                          const void* aux, void* y) {
+  __shared__ float red[4][8];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n = blockIdx.x;
+  const int U = d.K >> 4;
+  const bool chw = (d.flags & PG_LIN_IN_CHW) != 0;
+  const float* wr = w + (size_t)n * d.K;
+  for (int b0 = 0; b0 < d.B; b0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int u = wid * 64 + lane; u < U; u += 256) {
+      float wv[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t t = *reinterpret_cast<const f32x4_t*>(wr + u * 16 + 4 * j);
+        wv[4 * j] = t[0]; wv[4 * j + 1] = t[1]; wv[4 * j + 2] = t[2]; wv[4 * j + 3] = t[3];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int bb = b0 + q;
+        if (bb >= d.B) break;
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const size_t xi = chw ? ((size_t)bb * 16 + j) * d.in_cs + u : (size_t)bb * d.K + u * 16 + j;
+          s += wv[j] * LinIO<T>::ldx(d, x, xi);
+        }
+        acc[q] += s;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = wave_sum(acc[q]);
+    if (lane < 8) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q == lane) v = acc[q];
+      red[wid][lane] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 8 && b0 + (int)threadIdx.x < d.B) {
+      const int bb = b0 + threadIdx.x;
+      float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+      if (d.flags & PG_LIN_BIAS) v += b[n];
+      v *= d.scale;
+      if (d.flags & PG_LIN_LRELU) v = lrelu_f(v, d.slope);
+      const size_t yi = LinIO<T>::yidx(d, bb, n);
+      if (d.flags & PG_LIN_MASK) v *= lmask_f(LinIO<T>::ldy(d, aux, yi), d.slope);
+      LinIO<T>::sty(d, y, yi, v);
+    }
+    __syncthreads();
+  }
+}
+
+// Linear input gradient: block = 64 consecutive k (one per lane) x 16 waves splitting N,
+// batch rows in chunks of 8, partial sums reduced through LDS.
+template <typename T>
+__global__ __launch_bounds__(1024) void linear_dgrad_kernel3(pg_linear_desc d, const void* gy,
+                                                             const float* w, const void* aux,
+                                                             void* gx) {
+  __shared__ float red[16][8][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int n0 = (d.N * wid) / 16, n1 = (d.N * (wid + 1)) / 16;
+  for (int b0 = 0; b0 < d.B; b0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    if (k < d.K) {
+      int nn = n0;
+      for (; nn + 4 <= n1; nn += 4) {
+        float wv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wv[j] = w[(size_t)(nn + j) * d.K + k];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (b0 + q < d.B)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[q] += wv[j] * LinIO<T>::ldy(d, gy, LinIO<T>::yidx(d, b0 + q, nn + j));
+      }
+      for (; nn < n1; ++nn) {
+        const float wv = w[(size_t)nn * d.K + k];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (b0 + q < d.B) acc[q] += wv * LinIO<T>::ldy(d, gy, LinIO<T>::yidx(d, b0 + q, nn));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[wid][q][lane] = acc[q];
+    __syncthreads();
+    if (wid < 8) {
+      const int q = wid, bb = b0 + q;
+      if (bb < d.B && k < d.K) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc += red[r][q][lane];
+        sacc *= d.scale;
+        const size_t xi = LinIO<T>::xidx(d, bb, k);
+        if (d.flags & PG_LIN_MASK) sacc *= lmask_f(LinIO<T>::ldx(d, aux, xi), d.slope);
+        LinIO<T>::stx(d, gx, xi, sacc);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T>
 __global__ void linear_dgrad_kernel(pg_linear_desc d, const void* gy, const float* w,
                                     const void* aux, void* gx) {
@@ -1199,10 +1316,17 @@ int pg_linear_fwd(int dtype, const pg_linear_desc* d, const void* x, const float
   PG_CHECK_ARG(d && x && w && y && d->B > 0 && d->K > 0 && d->N > 0, "linear_fwd: bad args");
   PG_CHECK_ARG(!(d->flags & PG_LIN_BIAS) || b, "linear_fwd: BIAS without bias");
   PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_fwd: MASK without aux");
-  const int wpb = 4;
   hipStream_t st = (hipStream_t)stream;
-  DT_DISPATCH(dtype, linear_fwd_kernel, dim3(pg_cdiv(d->N, wpb)), dim3(64 * wpb), 0, st, *d, x, w, b,
-              aux, y);
+  // bf16: the coalesced kernels; f32 (the exact-parity mode) keeps the simple per-feature
+  // summation order, which the full-width parity tests pin (a different order moves
+  // near-zero leaky-relu inputs across the kink)
+  if (d->K % 16 == 0 && dtype == PG_BF16) {
+    DT_DISPATCH(dtype, linear_fwd_kernel2, dim3(d->N), dim3(256), 0, st, *d, x, w, b, aux, y);
+  } else {
+    const int wpb = 4;
+    DT_DISPATCH(dtype, linear_fwd_kernel, dim3(pg_cdiv(d->N, wpb)), dim3(64 * wpb), 0, st, *d, x,
+                w, b, aux, y);
+  }
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1214,8 +1338,13 @@ int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const fl
   const size_t n = (size_t)d->B * d->K;
   hipStream_t st = (hipStream_t)stream;
   (void)n;
-  DT_DISPATCH(dtype, linear_dgrad_kernel2, dim3(pg_cdiv(d->K, 64)), dim3(256), 0, st, *d, gy, w, aux,
-              gx);
+  if (dtype != PG_BF16) {
+    DT_DISPATCH(dtype, linear_dgrad_kernel2, dim3(pg_cdiv(d->K, 64)), dim3(256), 0, st, *d, gy, w,
+                aux, gx);
+  } else {
+    DT_DISPATCH(dtype, linear_dgrad_kernel3, dim3(pg_cdiv(d->K, 64)), dim3(1024), 0, st, *d, gy, w,
+                aux, gx);
+  }
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

@@ -107,12 +107,16 @@ class FlatParams:
         order = [n for n, _ in shapes if n not in dead] + [n for n, _ in shapes if n in dead]
         shp = dict(shapes)
         self.names = [n for n, _ in shapes]          # reference order
+        # every tensor starts on a 64-byte boundary (vector loads in the kernels); the
+        # padding slots stay zero (zero gradient -> Adam leaves them at zero)
         self.offsets, off = {}, 0
+        self.n_live = 0
         for n in order:
             self.offsets[n] = off
-            off += int(math.prod(shp[n]))
+            off += (int(math.prod(shp[n])) + 15) // 16 * 16
+            if n not in dead:
+                self.n_live = off
         self.numel = off
-        self.n_live = sum(int(math.prod(shp[n])) for n in order if n not in dead)
         self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.grad = torch.zeros_like(self.flat)
         self.m = torch.zeros_like(self.flat)

@@ -421,3 +421,36 @@ def test_conv_pack_batch(dtype):
     for (w, b, pf, pd, bs, sc), (rf, rd, rb) in zip(ents, refs):
         assert torch.equal(pf, rf) and torch.equal(pd, rd)
         assert torch.allclose(bs, rb, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B", [4, 11])
+def test_linear_paper_sizes(dtype, B):
+    """The mbstd linear (K = 16*512 CHW gather -> 512) and the latent layer (512 -> 16*512
+    CHW scatter) at the paper width, forward and input gradient."""
+    _L = lib()
+    hip, cpu = ops_pair(dtype)
+    C = 512
+    x = q(rnd(B, 4, 4, C, seed=71), dtype)
+    w = rnd(C, 16 * C, seed=72) * 0.05
+    bb = rnd(C, seed=73)
+    aux = q(rnd(B, 4, 4, C, seed=74), dtype)
+    gy = rnd(B, C, seed=75)
+    z = rnd(B, C, seed=76)
+    wf = rnd(16 * C, C, seed=77) * 0.05
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        r = {}
+        r["l1"] = torch.zeros(B, C, dtype=dt, device=dev)
+        ops.linear(x.to(dev).to(dt), w.to(dev), bb.to(dev), r["l1"], B=B,
+                   flags=_L.LIN_BIAS | _L.LIN_LRELU | _L.LIN_IN_CHW, scale=0.1)
+        r["gx"] = torch.zeros(B, 4, 4, C, dtype=dt, device=dev)
+        ops.linear_dgrad(gy.to(dev).to(dt), w.to(dev), r["gx"], B=B,
+                         flags=_L.LIN_IN_CHW | _L.LIN_MASK, scale=0.1, aux=aux.to(dev).to(dt))
+        r["f"] = torch.zeros(B, 4, 4, C, dtype=dt, device=dev)
+        ops.linear(z.to(dev), wf.to(dev), bb.repeat(16).to(dev), r["f"], B=B,
+                   flags=_L.LIN_BIAS | _L.LIN_LRELU | _L.LIN_OUT_CHW, scale=0.3)
+        res[dev] = r
+    for k in res["cpu"]:
+        cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 2e-5), k)
