@@ -67,6 +67,7 @@ for step in "$@"; do
           > gpurun_out/pmcq.log 2>&1
       rc=$?; echo "pmcq rc=$rc"; tail -n 3 gpurun_out/pmcq.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     listc) ( rocprofv3 -L > gpurun_out/counters.txt 2>&1 ); echo "listc rc=$?" ;;
+    opprof) run opprof 300 python tools/op_profile.py --json gpurun_out/opprof.json ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -20,7 +20,7 @@ from collections import defaultdict
 
 
 def family(name):
-    if "conv3x3_kernel" in name:
+    if "conv3x3_kernel" in name or "conv_hr_kernel" in name:
         return "conv3x3", True
     if "conv_splitk_epilogue" in name:
         return "conv3x3", False
