@@ -21,12 +21,17 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
 
 __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// round-to-nearest-even; NaN stays NaN
+// round-to-nearest-even; NaN stays NaN (v_cvt_pk_bf16_f32, one instruction per pair)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  bf16x2_t v;
+  v[0] = (__bf16)a;
+  v[1] = (__bf16)b;
+  return __builtin_bit_cast(uint32_t, v);
+}
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+  const __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
 }
 
 template <typename T> struct Ty;
@@ -53,8 +58,8 @@ template <> struct Ty<bf16_t> {
   }
   static __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
     u32x2_t q;
-    q[0] = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    q[1] = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    q[0] = pack_bf16x2(v[0], v[1]);
+    q[1] = pack_bf16x2(v[2], v[3]);
     *reinterpret_cast<u32x2_t*>(p) = q;
   }
 };

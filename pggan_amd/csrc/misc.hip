@@ -1047,6 +1047,8 @@ __global__ void cast_kernel(size_t n, const A* x, B* y) {
   GRID_STRIDE(i, n) Ty<B>::st(y + i, Ty<A>::ld(x + i));
 }
 
+#include "ew.inc"
+
 }  // namespace
 
 #define DT_DISPATCH(dtype, KERNEL, grid, block, shm, st, ...)                                  \
@@ -1068,9 +1070,14 @@ int pg_version(void) { return 100; }
 
 int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, void* stream) {
   PG_CHECK_ARG(x && y && npix > 0 && C % 4 == 0 && cs >= C && cs % 4 == 0, "pixnorm_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_pixnorm_fwd<float>(npix, C, cs, (const float*)x, (float*)y, st)
+                       : try_pixnorm_fwd<bf16_t>(npix, C, cs, (const bf16_t*)x, (bf16_t*)y, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   const int L = lanes_for(C);
   const size_t threads = (size_t)npix * L;
-  hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
     hipLaunchKernelGGL(pixnorm_fwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0, st,
                        npix, C, cs, L, (const float*)x, (float*)y);
@@ -1084,9 +1091,16 @@ int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, v
 int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, const void* gy,
                          float slope, int apply_mask, void* gz, void* stream) {
   PG_CHECK_ARG(u && gy && gz && npix > 0 && C % 4 == 0 && cs >= C, "pixnorm_lrelu_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_pixnorm_bwd<float>(npix, C, cs, (const float*)u, (const float*)gy, slope,
+                                                apply_mask, (float*)gz, st)
+                       : try_pixnorm_bwd<bf16_t>(npix, C, cs, (const bf16_t*)u, (const bf16_t*)gy,
+                                                 slope, apply_mask, (bf16_t*)gz, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   const int L = lanes_for(C);
   const size_t threads = (size_t)npix * L;
-  hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
     hipLaunchKernelGGL(pixnorm_lrelu_bwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0,
                        st, npix, C, cs, L, (const float*)u, (const float*)gy, slope, apply_mask,
@@ -1106,6 +1120,15 @@ int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* 
                "unpool_mask: bad args");
   const size_t n = (size_t)B * H * W * (C / 4);
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_unpool_mask<float>(B, H, W, C, g_cs, (const float*)g, y_cs,
+                                                (const float*)y, scale, slope, ups, out_cs,
+                                                (float*)out, st)
+                       : try_unpool_mask<bf16_t>(B, H, W, C, g_cs, (const bf16_t*)g, y_cs,
+                                                 (const bf16_t*)y, scale, slope, ups, out_cs,
+                                                 (bf16_t*)out, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (dtype == PG_F32)
     hipLaunchKernelGGL(unpool_mask_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        g_cs, (const float*)g, y_cs, (const float*)y, scale, slope, ups, out_cs,
@@ -1123,6 +1146,12 @@ int pg_avgpool2(int dtype, int B, int H, int W, int C, int x_cs, const void* x, 
   PG_CHECK_ARG(x && y && C % 4 == 0 && H % 2 == 0 && W % 2 == 0, "avgpool2: bad args");
   const size_t n = (size_t)B * (H / 2) * (W / 2) * (C / 4);
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_avgpool2<float>(B, H, W, C, x_cs, (const float*)x, y_cs, (float*)y, st)
+                       : try_avgpool2<bf16_t>(B, H, W, C, x_cs, (const bf16_t*)x, y_cs, (bf16_t*)y,
+                                              st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (dtype == PG_F32)
     hipLaunchKernelGGL(avgpool2_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        x_cs, (const float*)x, y_cs, (float*)y);
@@ -1137,6 +1166,12 @@ int pg_blend(int dtype, size_t n, float a, const void* x, float b, const void* y
              void* stream) {
   PG_CHECK_ARG(x && out, "blend: null pointer");
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_blend<float>(n, a, (const float*)x, b, (const float*)y, (float*)out, st)
+                       : try_blend<bf16_t>(n, a, (const bf16_t*)x, b, (const bf16_t*)y, (bf16_t*)out,
+                                           st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (dtype == PG_F32)
     hipLaunchKernelGGL(blend_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
                        (const float*)x, b, (const float*)y, (float*)out);
@@ -1154,6 +1189,14 @@ int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const fl
                "rgb_out: bad args");
   const size_t n = (size_t)B * R * R;
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32
+           ? try_rgb_out<float>(B, R, C, x_cs, (const float*)x, w, b, c, Cp, xp_cs, (const float*)xp,
+                                wp, bp, cp, alpha, img, st)
+           : try_rgb_out<bf16_t>(B, R, C, x_cs, (const bf16_t*)x, w, b, c, Cp, xp_cs,
+                                 (const bf16_t*)xp, wp, bp, cp, alpha, img, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (dtype == PG_F32)
     hipLaunchKernelGGL(rgb_out_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
                        (const float*)x, w, b, c, Cp, xp_cs, (const float*)xp, wp, bp, cp, alpha, img);
@@ -1174,6 +1217,10 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
                         float* dbp, hipStream_t st) {
   const float fa = xp ? alpha * c : c;
   size_t n = (size_t)B * R * R * (C / 4);
+  if (rgb_bwd_part<T>(B, R, C, x_cs, x, w, fa, 0, gimg, gx, dw, db, st) == 0) {
+    gx = nullptr;
+    dw = nullptr;
+  }
   if (gx)
     hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs, w,
                        fa, 0, gimg, gx);
@@ -1199,6 +1246,10 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     const int Rp = R / 2;
     const float fp = (1.f - alpha) * cp;
     n = (size_t)B * Rp * Rp * (Cp / 4);
+    if (rgb_bwd_part<T>(B, Rp, Cp, xp_cs, xp, wp, fp, 1, gimg, gxp, dwp, dbp, st) == 0) {
+      gxp = nullptr;
+      dwp = nullptr;
+    }
     if (gxp)
       hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, Rp, Cp, xp_cs,
                          wp, fp, 1, gimg, gxp);
@@ -1244,6 +1295,13 @@ int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, cons
   PG_CHECK_ARG(img && w && y && C % 4 == 0 && y_cs >= C, "from_rgb: bad args");
   const size_t n = (size_t)B * R * R * (C / 4);
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_from_rgb<float>(B, R, C, img, down, w, b, c, slope, (const float*)mask_y,
+                                             y_cs, (float*)y, st)
+                       : try_from_rgb<bf16_t>(B, R, C, img, down, w, b, c, slope,
+                                              (const bf16_t*)mask_y, y_cs, (bf16_t*)y, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (dtype == PG_F32)
     hipLaunchKernelGGL(from_rgb_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
                        down, w, b, c, slope, (const float*)mask_y, y_cs, (float*)y);
@@ -1260,6 +1318,13 @@ int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, 
   PG_CHECK_ARG(w && gz && C % 4 == 0, "from_rgb_bwd: bad args");
   PG_CHECK_ARG(!(dw || db) || img, "from_rgb_bwd: wgrad needs img");
   hipStream_t st = (hipStream_t)stream;
+  if ((dtype == PG_F32 ? try_from_rgb_bwd<float>(B, R, C, img, down, w, c, gz_cs, (const float*)gz,
+                                                 gimg, dw, db, st)
+                       : try_from_rgb_bwd<bf16_t>(B, R, C, img, down, w, c, gz_cs,
+                                                  (const bf16_t*)gz, gimg, dw, db, st)) == 0) {
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (gimg) {
     const int Ri = down ? 2 * R : R;
     const size_t n = (size_t)B * Ri * Ri;
@@ -1304,6 +1369,12 @@ int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, 
 
 int pg_img_fade(int B, int C, int R, const float* x, float alpha, float* out, void* stream) {
   PG_CHECK_ARG(x && out && R % 2 == 0, "img_fade: bad args");
+  if (R % 4 == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)out & 7) == 0) {
+    const dim3 grid((R / 2 + 255) / 256, B * C * (R / 2));
+    hipLaunchKernelGGL(img_fade_v, grid, dim3(256), 0, (hipStream_t)stream, R, x, alpha, out);
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   const size_t n = (size_t)B * C * R * R;
   hipLaunchKernelGGL(img_fade_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, B, C, R,
                      x, alpha, out);

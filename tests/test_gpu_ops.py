@@ -454,3 +454,82 @@ def test_linear_paper_sizes(dtype, B):
         res[dev] = r
     for k in res["cpu"]:
         cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 2e-5), k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,H", [(16, 512), (32, 256), (64, 64), (512, 4), (24, 8)])
+def test_elementwise_vector_shapes(dtype, C, H):
+    """The vectorised row-grid kernels (ew.inc) at stage shapes: rows wider than one
+    256-thread block, 16..512 channels, and a non-power-of-two count (generic fallback)."""
+    hip, cpu = ops_pair(dtype)
+    B = 2
+    x = q(rnd(B, H, H, C, seed=51), dtype)
+    g = q(rnd(B, H // 2, H // 2, C, seed=52), dtype)
+    y = q(rnd(B, H, H, C, seed=53), dtype)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        X, G, Y = x.to(dev).to(dt), g.to(dev).to(dt), y.to(dev).to(dt)
+        r = {}
+        r["pn"] = torch.zeros_like(X); ops.pixnorm(X, r["pn"], C)
+        r["pnb"] = torch.zeros_like(X); ops.pixnorm_lrelu_bwd(X, Y, r["pnb"], C, 0.2)
+        r["um"] = torch.zeros_like(X)
+        ops.unpool_mask(G, Y, r["um"], B=B, H=H, W=H, C=C, scale=0.25, slope=0.2, ups=True)
+        r["um0"] = torch.zeros_like(X)
+        ops.unpool_mask(X, Y, r["um0"], B=B, H=H, W=H, C=C, scale=0.5, slope=0.2, ups=False)
+        r["ap"] = torch.zeros_like(G); ops.avgpool2(X, r["ap"], B=B, H=H, W=H, C=C)
+        r["bl"] = torch.zeros_like(X); ops.blend(0.3, X, 0.7, Y, r["bl"])
+        res[dev] = r
+    for k in res["cpu"]:
+        cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 1e-6), f"{k} C={C} H={H}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,Cp,R", [(32, 64, 512), (16, 32, 1024), (64, 128, 64)])
+def test_rgb_vector_shapes(dtype, C, Cp, R):
+    """to/fromRGB kernels at the 512^2/1024^2 stage widths (row grids wider than a block)."""
+    hip, cpu = ops_pair(dtype)
+    B = 1
+    x = q(rnd(B, R, R, C, seed=61), dtype)
+    xp = q(rnd(B, R // 2, R // 2, Cp, seed=62), dtype)
+    w, b = rnd(3, C, 1, 1, seed=63), rnd(3, seed=64)
+    wp, bp = rnd(3, Cp, 1, 1, seed=65), rnd(3, seed=66)
+    gimg = rnd(B, 3, R, R, seed=67)
+    img = rnd(B, 3, R, R, seed=68)
+    fw, fb = rnd(C, 3, 1, 1, seed=69), rnd(C, seed=70)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        X, XP = x.to(dev).to(dt), xp.to(dev).to(dt)
+        r = {"img": torch.zeros(B, 3, R, R, device=dev)}
+        ops.rgb_out(X, w.to(dev), b.to(dev), 0.35, r["img"], B=B, R=R, C=C, xp=XP, wp=wp.to(dev),
+                    bp=bp.to(dev), cp=0.2, Cp=Cp, alpha=0.3)
+        r["gx"] = torch.zeros_like(X)
+        r["dw"] = torch.zeros(3, C, 1, 1, device=dev)
+        r["db"] = torch.zeros(3, device=dev)
+        r["gxp"] = torch.zeros_like(XP)
+        r["dwp"] = torch.zeros(3, Cp, 1, 1, device=dev)
+        r["dbp"] = torch.zeros(3, device=dev)
+        ops.rgb_out_bwd(X, w.to(dev), 0.35, gimg.to(dev), r["gx"], r["dw"], r["db"], B=B, R=R, C=C,
+                        xp=XP, wp=wp.to(dev), cp=0.2, Cp=Cp, alpha=0.3, gxp=r["gxp"], dwp=r["dwp"],
+                        dbp=r["dbp"])
+        for down in (False, True):
+            Ro = R // 2 if down else R
+            yy = torch.zeros(B, Ro, Ro, C, dtype=dt, device=dev)
+            ops.from_rgb(img.to(dev), fw.to(dev), fb.to(dev), 0.8, yy, B=B, R=Ro, C=C, down=down)
+            r[f"fr{down}"] = yy
+            gi = torch.zeros(B, 3, R, R, device=dev)
+            dw_ = torch.zeros(C, 3, 1, 1, device=dev)
+            db_ = torch.zeros(C, device=dev)
+            ops.from_rgb_bwd(yy, fw.to(dev), 0.8, B=B, R=Ro, C=C, down=down, img=img.to(dev),
+                             gimg=gi, dw=dw_, db=db_)
+            r[f"fgi{down}"], r[f"fdw{down}"], r[f"fdb{down}"] = gi, dw_, db_
+        fo = torch.zeros_like(img.to(dev))
+        ops.img_fade(img.to(dev), 0.4, fo)
+        r["fade"] = fo
+        res[dev] = r
+    for k in res["cpu"]:
+        # fp32 weight gradients sum ~1M pixel terms in a different order: 3e-4
+        cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 3e-4), f"{k} C={C} R={R}")
