@@ -51,6 +51,12 @@ int pg_version(void);
 #define PG_CONV_MASK 8    /* multiply by lrelu'(aux) (aux at output resolution, channel stride aux_cs) */
 #define PG_CONV_POOL 16   /* 2x2 pool of the activated result (avg: out_scale=0.25, sum: 1.0) */
 #define PG_CONV_ACCUM 32  /* y += result */
+/* PixelNorm fused into the epilogue (lib/layers.py:8-14 applied after the conv+LReLU of a
+ * generator block, lib/blocks.py:128-129,138-139): y = v * rsqrt(mean_c v^2 + 1e-8) with v
+ * the activated result rounded to the storage dtype; if y2 != NULL it receives the
+ * per-pixel factor rsqrt(...) as fp32 [B*H*W] (for pg_pixnorm_lrelu_bwd_y).  Needs every
+ * output channel in one tile: query pg_conv3x3_supported().  Not with POOL/MASK/ACCUM. */
+#define PG_CONV_PIXNORM 64
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -89,6 +95,9 @@ size_t pg_conv3x3_workspace_size(const pg_conv_desc* d);
 int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                    const float* bias, const void* aux, void* y, void* y2, void* ws,
                    size_t ws_bytes, void* stream);
+/* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
+ * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
+int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);
 /* weight gradient, accumulates: dw[o][c][ky][kx] += scale * sum_p gz[p][o] * x[p+tap][c]
  * and, if db != NULL, the bias gradient db[o] += scale * sum_p gz[p][o] (fused: gz is read
  * once).  desc: B,H,W, cin, cout, x_cs, y_cs = gz channel stride, flags may hold
@@ -111,6 +120,10 @@ int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, cons
 
 /* ---- elementwise helpers (NHWC, channel stride cs) */
 /* out[p] = scale * g[ups ? p/2 : p] * (y ? lrelu'(y[p]) : 1)   (avg-pool backward, lib/blocks.py:193) */
+/* the same backward from the fused conv's outputs (PG_CONV_PIXNORM): y = normalised
+ * activation, r = per-pixel factor (fp32 [npix]); u = y / r is never stored */
+int pg_pixnorm_lrelu_bwd_y(int dtype, int npix, int C, int cs, const void* y, const float* r,
+                           const void* gy, float slope, void* gz, void* stream);
 int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
                    const void* y, float scale, float slope, int ups, int out_cs, void* out,
                    void* stream);

@@ -16,6 +16,7 @@ import torch
 PG_F32, PG_BF16 = 0, 1
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
+CONV_PIXNORM = 64
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
     1, 2, 4, 8, 16, 32, 64)
@@ -58,12 +59,14 @@ _SIGS = {
     "pg_conv3x3_workspace_size": ([ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
                        _I),
+    "pg_conv3x3_supported": ([_I, ctypes.POINTER(ConvDesc), _SZ], _I),
     "pg_conv3x3_wgrad_workspace_size": ([_I, ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP],
                          _I),
     "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
+    "pg_pixnorm_lrelu_bwd_y": ([_I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _VP], _I),
     "pg_unpool_mask": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _F, _F, _I, _I, _VP, _VP], _I),
     "pg_avgpool2": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _VP], _I),
     "pg_blend": ([_I, _SZ, _F, _VP, _F, _VP, _VP, _VP], _I),
@@ -187,6 +190,11 @@ class HipOps:
                                           _p(aux), _p(y), _p(y2), _p(ws), wsb, self._s()),
                   "conv3x3_fwd")
 
+    def conv_supported(self, *, B, H, W, cin, cout, flags, ws_bytes=0):
+        """Whether the conv kernel picked for this shape supports `flags` (fused epilogues)."""
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, flags, 0.2, 1.0)
+        return bool(self.lib.pg_conv3x3_supported(self.dt, ctypes.byref(d), ws_bytes))
+
     def conv_workspace_bytes(self, *, B, H, W, cin, cout):
         d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, 0, 0.0, 1.0)
         return int(self.lib.pg_conv3x3_workspace_size(ctypes.byref(d)))
@@ -224,6 +232,15 @@ class HipOps:
         self._chk(self.lib.pg_pixnorm_lrelu_bwd(self._dt(u), npix, C, u.shape[-1], _p(u), _p(gy),
                                                 slope, 1 if mask else 0, _p(gz), self._s()),
                   "pixnorm_lrelu_bwd")
+
+    def pixnorm_lrelu_bwd_y(self, y, r, gy, gz, C, slope):
+        """Backward of lrelu -> PixelNorm from the fused conv's normalised output y and its
+        per-pixel factor r (fp32, one per pixel)."""
+        self._cuda(y, r, gy, gz)
+        npix = y.numel() // y.shape[-1]
+        self._chk(self.lib.pg_pixnorm_lrelu_bwd_y(self._dt(y), npix, C, y.shape[-1], _p(y), _p(r),
+                                                  _p(gy), slope, _p(gz), self._s()),
+                  "pixnorm_lrelu_bwd_y")
 
     # -- elementwise -------------------------------------------------------
     def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):

@@ -221,6 +221,45 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
     // wave-instruction writes 16 pixels x 4 lane-groups x 8 B = whole pixel rows
     const bool has_bias = !p.ws && (p.flags & PG_CONV_BIAS) != 0;
     const bool do_lrelu = !p.ws && (p.flags & PG_CONV_LRELU) != 0;
+    if (p.flags & PG_CONV_PIXNORM) {
+      // PixelNorm over the cout channels of each pixel (WN == 1, n0 == 0, cout_p <= BN)
+      T* y = reinterpret_cast<T*>(p.y);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int pm = wm * (BM / WM) + mt * 16 + r;
+        const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+        const int b = b0 + nb;
+        const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
+        float v[NT][4];
+        float ss = 0.f;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = nt * 16 + 4 * g + j;
+            float u = acc[mt][nt][j] + ((has_bias && n < p.cout) ? p.bias[n] : 0.f);
+            if (do_lrelu) u = lrelu_f(u, p.slope);
+            if constexpr (sizeof(T) == 2) u = bf2f(f2bf(u));   // as stored
+            v[nt][j] = n < p.cout ? u : 0.f;
+            ss += v[nt][j] * v[nt][j];
+          }
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        const float rn = rsqrtf(ss / (float)p.cout + 1e-8f);
+        if (b >= p.B) continue;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int n = nt * 16 + 4 * g;
+          if (n >= p.cout) continue;
+          float o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = v[nt][j] * rn;
+          Ty<T>::st4(y + pix * p.y_cs + n, o);
+        }
+        if (p.y2 && g == 0) reinterpret_cast<float*>(p.y2)[pix] = rn;
+      }
+      return;
+    }
     const bool do_mask = (p.flags & PG_CONV_MASK) != 0;
     const bool do_acc = (p.flags & PG_CONV_ACCUM) != 0;
     const bool pool = !p.ws && (p.flags & PG_CONV_POOL) != 0;
@@ -1238,9 +1277,27 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 
 #include "conv_hr.inc"
 
+// Which fused epilogues the kernel the dispatcher picks supports.
+template <typename T>
+bool conv_supported(const pg_conv_desc* d, size_t wsb) {
+  if (!(d->flags & PG_CONV_PIXNORM)) return true;
+  if (d->flags & (PG_CONV_POOL | PG_CONV_MASK | PG_CONV_ACCUM)) return false;
+  const int cout_p = (d->cout + 15) & ~15;
+  if constexpr (sizeof(T) == 2) {
+    if (conv_hr_ok(d)) return cout_p <= conv_hr_bn(d);
+  }
+  int BM, BN;
+  conv_tile_for(d->cout, &BM, &BN, d->W);
+  const size_t need = conv_ws_bytes(d);
+  const bool split = need && wsb >= need && conv_splits(d) > 1;
+  return BN <= 32 && cout_p <= BN && !split;   // [cout][pixel] variants, single pass
+}
+
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                   const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
+  PG_CHECK_ARG(conv_supported<T>(d, wsb), "conv3x3_fwd: flags 0x%x not supported for cout %d at %dx%d",
+               d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
     if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, st);
   }
@@ -1323,11 +1380,18 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
                "conv3x3_fwd: MASK flag without aux");
   PG_CHECK_ARG(!((d->flags & PG_CONV_MASK) && (d->flags & PG_CONV_POOL)),
                "conv3x3_fwd: MASK and POOL together are not supported");
-  PG_CHECK_ARG(!y2 || (d->flags & PG_CONV_POOL), "conv3x3_fwd: y2 only with POOL");
+  PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM)),
+               "conv3x3_fwd: y2 only with POOL or PIXNORM");
   PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
   return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
+}
+
+int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes) {
+  if (!d) return 0;
+  return (dtype == PG_F32 ? conv_supported<float>(d, ws_bytes) : conv_supported<bf16_t>(d, ws_bytes))
+             ? 1 : 0;
 }
 
 size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d) {

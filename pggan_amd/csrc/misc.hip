@@ -1113,6 +1113,21 @@ int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, cons
   return PG_OK;
 }
 
+int pg_pixnorm_lrelu_bwd_y(int dtype, int npix, int C, int cs, const void* y, const float* r,
+                           const void* gy, float slope, void* gz, void* stream) {
+  PG_CHECK_ARG(y && r && gy && gz && npix > 0 && C > 0 && cs >= C, "pixnorm_lrelu_bwd_y: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const int rc = dtype == PG_F32
+                     ? try_pixnorm_bwd_y<float>(npix, C, cs, (const float*)y, r, (const float*)gy,
+                                                slope, (float*)gz, st)
+                     : try_pixnorm_bwd_y<bf16_t>(npix, C, cs, (const bf16_t*)y, r,
+                                                 (const bf16_t*)gy, slope, (bf16_t*)gz, st);
+  PG_CHECK_ARG(rc == 0, "pixnorm_lrelu_bwd_y: C=%d (stride %d) needs a power-of-two count of 16-byte vectors <= 64",
+               C, cs);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
 int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
                    const void* y, float scale, float slope, int ups, int out_cs, void* out,
                    void* stream) {

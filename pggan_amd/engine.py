@@ -170,6 +170,7 @@ class StepEngine:
         self.d0 = d[0]
         self.mcs = cinp(d[0] + 1)
         self.keep_fake_D = False
+        self.fuse_pixnorm = True   # PixelNorm in the G conv epilogues where the kernel allows
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
         self._alloc()
@@ -193,6 +194,9 @@ class StepEngine:
             Ri = 8 * 2 ** i
             for k in ("ua", "ya", "ub", "yb", "gzb", "gya", "gza"):
                 g[f"{k}{i}"] = t(B, Ri, Ri, d[i + 1])
+            # per-pixel PixelNorm factors of the fused conv epilogues (G-half backward)
+            g[f"ra{i}"] = t(B, Ri, Ri, 1, f32=True)
+            g[f"rb{i}"] = t(B, Ri, Ri, 1, f32=True)
         g["img"] = t(B, 3, R, R, f32=True)
         # gradient wrt level outputs: lvl 0 = y0 (4x4), lvl i+1 = yb_i
         for j in range(s + 1):
@@ -341,8 +345,37 @@ class StepEngine:
         self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c,
                             db=db, ws=self.ws if need else None)
 
+    def _pn_fused(self, H, cin, cout, flags):
+        """Whether this generator conv can run PixelNorm in its epilogue (all output
+        channels in one tile of the kernel the library picks for the shape)."""
+        key = ("pn", H, cin, cout, flags)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            need = self._ws_need("c", H, cin, cout, False)
+            self._ws_cache[key] = bool(self.fuse_pixnorm and f is not None and
+                                       f(B=self.B, H=H, W=H, cin=cin, cout=cout,
+                                         flags=flags | L.CONV_PIXNORM | L.CONV_BIAS,
+                                         ws_bytes=need))
+        return self._ws_cache[key]
+
+    def _g_conv_pn(self, key, x, u, y, r, H, cin, cout, flags, keep):
+        """conv + lrelu + PixelNorm of a generator block (lib/blocks.py:126-139): fused
+        (y and, for the backward, the per-pixel factor r) or conv -> u then pixnorm -> y."""
+        if self._pn_fused(H, cin, cout, flags):
+            self._conv("G", key, x, y, H, cin, cout, flags | L.CONV_PIXNORM, y2=r if keep else None)
+        else:
+            self._conv("G", key, x, u, H, cin, cout, flags)
+            self.ops.pixnorm(u, y, cout)
+
+    def _g_pn_bwd(self, key, u, y, r, gy, gz, H, cin, cout, flags):
+        if self._pn_fused(H, cin, cout, flags):
+            self.ops.pixnorm_lrelu_bwd_y(y, r, gy, gz, cout, SLOPE)
+        else:
+            self.ops.pixnorm_lrelu_bwd(u, gy, gz, cout, SLOPE)
+
     # ================================================================== G
-    def g_forward(self, P, z, alpha):
+    def g_forward(self, P, z, alpha, keep=True):
+        """keep: store what g_backward needs (the G half); the D half only needs the image."""
         ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
         if z is not g["z"]:
             g["z"].copy_(z)
@@ -357,11 +390,10 @@ class StepEngine:
         prev = g["y0"]
         for i in range(s):                                                   # nets.py:144-149
             Ri = 8 * 2 ** i
-            self._conv("G", f"a{i}", prev, g[f"ua{i}"], Ri, d[i], d[i + 1],
-                       L.CONV_UPS_IN | L.CONV_LRELU)
-            ops.pixnorm(g[f"ua{i}"], g[f"ya{i}"], d[i + 1])
-            self._conv("G", f"b{i}", g[f"ya{i}"], g[f"ub{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
-            ops.pixnorm(g[f"ub{i}"], g[f"yb{i}"], d[i + 1])
+            self._g_conv_pn(f"a{i}", prev, g[f"ua{i}"], g[f"ya{i}"], g[f"ra{i}"], Ri, d[i],
+                            d[i + 1], L.CONV_UPS_IN | L.CONV_LRELU, keep)
+            self._g_conv_pn(f"b{i}", g[f"ya{i}"], g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], Ri,
+                            d[i + 1], d[i + 1], L.CONV_LRELU, keep)
             prev = g[f"yb{i}"]
         self._rgb_out(P, alpha)
         return g["img"]
@@ -394,13 +426,15 @@ class StepEngine:
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
-            ops.pixnorm_lrelu_bwd(g[f"ub{i}"], g[f"gy{i + 1}"], g[f"gzb{i}"], d[i + 1], SLOPE)
+            self._g_pn_bwd(f"b{i}", g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], g[f"gy{i + 1}"],
+                           g[f"gzb{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
                         d[i + 1],
                         db=GR[b + "bias"])
             self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gya{i}"], Ri, d[i + 1], d[i + 1], 0,
                        dgrad=True)
-            ops.pixnorm_lrelu_bwd(g[f"ua{i}"], g[f"gya{i}"], g[f"gza{i}"], d[i + 1], SLOPE)
+            self._g_pn_bwd(f"a{i}", g[f"ua{i}"], g[f"ya{i}"], g[f"ra{i}"], g[f"gya{i}"],
+                           g[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_UPS_IN | L.CONV_LRELU)
             self._wgrad("G", f"a{i}", self._ylvl(i), g[f"gza{i}"], GR[a + "weight"], Ri, d[i],
                         d[i + 1], ups=True,
                         db=GR[a + "bias"])
@@ -595,7 +629,7 @@ class StepEngine:
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
             self.d_backward(PD, GD, D["u"], alpha_D, img=xr)
         # ---- fake
-        img_fake = self.g_forward(PG, z, alpha_G)                               # :226-227
+        img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
         if self.keep_fake_D:
             img_fake = img_fake.clone()
         self.d_forward(PD, img_fake, alpha_D)                                   # :228

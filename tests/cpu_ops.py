@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as F
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
+CONV_PIXNORM = 64
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW = 1, 2, 4, 8, 16
 
 
@@ -53,9 +54,13 @@ def mbstd_ref(x):
 
 
 class CpuOps:
-    def __init__(self, dtype=torch.float32):
+    def __init__(self, dtype=torch.float32, fused=True):
         assert dtype == torch.float32
         self.tdtype = dtype
+        self.fused = fused          # report the fused conv epilogues as supported
+
+    def conv_supported(self, *, B, H, W, cin, cout, flags, ws_bytes=0):
+        return self.fused or not (flags & CONV_PIXNORM)
 
     # -- conv ------------------------------------------------------------
     def packed_elems(self, mode, cout, cin):
@@ -90,6 +95,11 @@ class CpuOps:
         if flags & CONV_LRELU:
             z = F.leaky_relu(z, slope)
         z = z.permute(0, 2, 3, 1)                       # NHWC [B,H,W,cout]
+        if flags & CONV_PIXNORM:
+            r = ((z * z).mean(-1, keepdim=True) + 1e-8).rsqrt()
+            z = z * r
+            if y2 is not None:
+                y2.view(B, H, W)[...] = r[..., 0]
         if flags & CONV_POOL:
             if y2 is not None:
                 y2[..., :cout] = z
@@ -129,6 +139,11 @@ class CpuOps:
         if mask:
             o = o * lmask(a, slope)
         gz[..., :C] = o
+
+    def pixnorm_lrelu_bwd_y(self, y, r, gy, gz, C, slope):
+        a, b = y[..., :C], gy[..., :C]
+        rr = r.reshape(a.shape[:-1] + (1,))
+        gz[..., :C] = rr * (b - a * (a * b).mean(-1, keepdim=True)) * lmask(a, slope)
 
     # -- elementwise -------------------------------------------------------
     def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):

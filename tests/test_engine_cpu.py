@@ -106,3 +106,13 @@ def test_engine_schedule_matches_reference(name):
     eng, fpG, fpD = build(meta, CpuOps())
     tol = 1e-4 if name.startswith("tiny") else 1e-3   # full width: K=4608 fp32 sums
     run_and_check(meta, z, eng, fpG, fpD, torch.from_numpy, tol=tol, ptol=1e-6)
+
+
+def test_engine_schedule_unfused_pixelnorm():
+    """The unfused generator path (conv -> u, separate PixelNorm kernel, backward from u)
+    that the engine takes where the conv tile cannot hold every output channel."""
+    torch.set_num_threads(4)
+    name = [n for n in NAMES if n.startswith("tiny")][-1]
+    meta, z = load(name)
+    eng, fpG, fpD = build(meta, CpuOps(fused=False))
+    run_and_check(meta, z, eng, fpG, fpD, torch.from_numpy, tol=1e-4, ptol=1e-6)
