@@ -57,6 +57,17 @@ int pg_version(void);
  * per-pixel factor rsqrt(...) as fp32 [B*H*W] (for pg_pixnorm_lrelu_bwd_y).  Needs every
  * output channel in one tile: query pg_conv3x3_supported().  Not with POOL/MASK/ACCUM. */
 #define PG_CONV_PIXNORM 64
+/* Sign-bit masks (bf16, the H,W >= 16 kernel; query pg_conv3x3_supported).  A bit tensor
+ * holds the leaky-relu sign (activation > 0) of every channel: [B][H][W][bytes], channel c
+ * at byte c/8, bit c%8.  1 bit replaces a 16-bit activation wherever only its sign is read
+ * again (the discriminator's conv+LReLU+pool outputs, lib/blocks.py:189-193). */
+#define PG_CONV_Y2_BITS 128   /* with POOL: y2 receives the sign bits of the pre-pool output */
+#define PG_CONV_AUX_BITS 256  /* MASK operand aux is a bit tensor (aux_cs = bytes per pixel);
+                                 with POOL the mask applies before pooling */
+#define PG_CONV_X_BITS 512    /* x is masked on load by lrelu'(xbits) at conv resolution
+                                 (pg_conv3x3_fwd_ex; xb_cs = bytes per pixel) */
+#define PG_CONV_GZ_BITS 1024  /* wgrad: gz is at H/2 x W/2 and the effective gradient is
+                                 up2(gz) * lrelu'(gzbits) (pg_conv3x3_wgrad_ex) */
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -65,6 +76,7 @@ typedef struct {
   int flags;
   float slope;     /* leaky relu slope */
   float out_scale;
+  int xb_cs;       /* bytes per pixel of the X_BITS / GZ_BITS bit tensor */
 } pg_conv_desc;
 
 #define PG_PACK_FWD 0    /* wpk[cout_p][9][cin_p]   = scale * W[o][c][tap]          */
@@ -95,6 +107,10 @@ size_t pg_conv3x3_workspace_size(const pg_conv_desc* d);
 int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                    const float* bias, const void* aux, void* y, void* y2, void* ws,
                    size_t ws_bytes, void* stream);
+/* pg_conv3x3_fwd with the input-mask bit tensor of PG_CONV_X_BITS */
+int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
+                      const void* wpk, const float* bias, const void* aux, void* y, void* y2,
+                      void* ws, size_t ws_bytes, void* stream);
 /* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
  * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);
@@ -108,6 +124,11 @@ int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);
 size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d);
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
                      float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
+/* pg_conv3x3_wgrad with PG_CONV_GZ_BITS: gz at half resolution (channel stride y_cs),
+ * gzbits at full resolution (xb_cs bytes per pixel); bf16 only */
+int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const void* gz,
+                        const void* gzbits, float scale, float* dw, float* db, void* ws,
+                        size_t ws_bytes, void* stream);
 /* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
                  void* stream);

@@ -17,6 +17,7 @@ PG_F32, PG_BF16 = 0, 1
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
 CONV_PIXNORM = 64
+CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
     1, 2, 4, 8, 16, 32, 64)
@@ -28,7 +29,7 @@ LIB_PATH = os.path.join(_HERE, "libpggan_hip.so")
 class ConvDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
                 ("B", "H", "W", "cin", "cout", "x_cs", "y_cs", "aux_cs", "y2_cs", "flags")] + \
-               [("slope", ctypes.c_float), ("out_scale", ctypes.c_float)]
+               [("slope", ctypes.c_float), ("out_scale", ctypes.c_float), ("xb_cs", ctypes.c_int)]
 
 
 class PackItem(ctypes.Structure):
@@ -60,6 +61,10 @@ _SIGS = {
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
                        _I),
     "pg_conv3x3_supported": ([_I, ctypes.POINTER(ConvDesc), _SZ], _I),
+    "pg_conv3x3_fwd_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
+                           _SZ, _VP], _I),
+    "pg_conv3x3_wgrad_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _F, _VP, _VP, _VP, _SZ,
+                             _VP], _I),
     "pg_conv3x3_wgrad_workspace_size": ([_I, ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP],
                          _I),
@@ -179,38 +184,48 @@ class HipOps:
                   "conv3x3_pack_batch")
 
     def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
-                bias=None, aux=None, y2=None, ws=None):
-        """ws: optional fp32 workspace tensor enabling split-K (see conv_workspace_bytes)."""
-        self._cuda(x, wpk, y, bias, aux, y2, ws)
+                bias=None, aux=None, y2=None, ws=None, xbits=None):
+        """ws: optional fp32 workspace tensor enabling split-K (see conv_workspace_bytes).
+        Bit tensors (aux with CONV_AUX_BITS, y2 with CONV_Y2_BITS, xbits with CONV_X_BITS)
+        are uint8 [B, H, W, bytes per pixel]."""
+        self._cuda(x, wpk, y, bias, aux, y2, ws, xbits)
         d = ConvDesc(B, H, W, cin, cout, x.shape[-1], y.shape[-1],
                      aux.shape[-1] if aux is not None else 0,
-                     y2.shape[-1] if y2 is not None else 0, flags, slope, out_scale)
+                     y2.shape[-1] if y2 is not None else 0, flags, slope, out_scale,
+                     xbits.shape[-1] if xbits is not None else 0)
         wsb = ws.numel() * ws.element_size() if ws is not None else 0
-        self._chk(self.lib.pg_conv3x3_fwd(self._dt(y), ctypes.byref(d), _p(x), _p(wpk), _p(bias),
-                                          _p(aux), _p(y), _p(y2), _p(ws), wsb, self._s()),
+        self._chk(self.lib.pg_conv3x3_fwd_ex(self._dt(y), ctypes.byref(d), _p(x), _p(xbits),
+                                             _p(wpk), _p(bias), _p(aux), _p(y), _p(y2), _p(ws),
+                                             wsb, self._s()),
                   "conv3x3_fwd")
 
     def conv_supported(self, *, B, H, W, cin, cout, flags, ws_bytes=0):
         """Whether the conv kernel picked for this shape supports `flags` (fused epilogues)."""
-        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, flags, 0.2, 1.0)
+        if flags & CONV_GZ_BITS:       # the weight-gradient operand form (bf16 kernel only)
+            return self.dt == PG_BF16 and H % 2 == 0 and W % 2 == 0 and cout % 8 == 0
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, flags, 0.2, 1.0, 0)
         return bool(self.lib.pg_conv3x3_supported(self.dt, ctypes.byref(d), ws_bytes))
 
     def conv_workspace_bytes(self, *, B, H, W, cin, cout):
-        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, 0, 0.0, 1.0)
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, 0, 0.0, 1.0, 0)
         return int(self.lib.pg_conv3x3_workspace_size(ctypes.byref(d)))
 
     def wgrad_workspace_bytes(self, *, B, H, W, cin, cout, ups=False):
-        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, CONV_UPS_IN if ups else 0, 0.0, 1.0)
+        d = ConvDesc(B, H, W, cin, cout, 0, 0, 0, 0, CONV_UPS_IN if ups else 0, 0.0, 1.0, 0)
         return int(self.lib.pg_conv3x3_wgrad_workspace_size(self.dt, ctypes.byref(d)))
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None):
-        """ws: optional fp32 workspace (see wgrad_workspace_bytes) for split reductions."""
-        self._cuda(x, gz, dw, db, ws)
-        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0,
-                     CONV_UPS_IN if ups else 0, 0.0, 1.0)
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None,
+                   gzbits=None, slope=0.2):
+        """ws: optional fp32 workspace (see wgrad_workspace_bytes) for split reductions.
+        gzbits: the gradient is up2(gz) * lrelu'(gzbits) (gz at H/2, bits uint8 at H)."""
+        self._cuda(x, gz, dw, db, ws, gzbits)
+        fl = (CONV_UPS_IN if ups else 0) | (CONV_GZ_BITS if gzbits is not None else 0)
+        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0, fl, slope, 1.0,
+                     gzbits.shape[-1] if gzbits is not None else 0)
         wsb = ws.numel() * ws.element_size() if ws is not None else 0
-        self._chk(self.lib.pg_conv3x3_wgrad(self._dt(gz), ctypes.byref(d), _p(x), _p(gz), scale,
-                                            _p(dw), _p(db), _p(ws), wsb, self._s()),
+        self._chk(self.lib.pg_conv3x3_wgrad_ex(self._dt(gz), ctypes.byref(d), _p(x), _p(gz),
+                                               _p(gzbits), scale, _p(dw), _p(db), _p(ws), wsb,
+                                               self._s()),
                   "conv3x3_wgrad")
 
     def bias_grad(self, g, db, C, scale):

@@ -42,6 +42,9 @@ struct ConvParams {
   float* ws;
   int cps;
   size_t slab;   // elements per slab = B*H*W*cout_p
+  // PG_CONV_X_BITS: sign bits masking the input on load ([B][H][W][xb_cs bytes], conv res)
+  const unsigned char* xbits;
+  int xb_cs;
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
@@ -670,6 +673,10 @@ struct WgBParams {
   float scale;
   int NB, TH, TW, tiles_x, tiles_y, ntiles, tiles_per_split;
   int GZS, HS, halo_elems;
+  // PG_CONV_GZ_BITS: gz at half resolution, masked by lrelu'(gzb) at full resolution
+  const unsigned char* gzb;
+  int gzb_cs;
+  float slope;
 };
 
 constexpr int WGB_BP = 128;        // pixels per staged tile
@@ -678,7 +685,7 @@ constexpr int WGB_MAXHALO = 288;   // max halo pixels of a 128-pixel tile (pick_
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <int MO, int NC, int WMO, int WNC, int PD, int WPE>
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void wgrad_bf16_kernel(WgBParams p) {
   constexpr int KW = 4 / (WMO * WNC);
@@ -719,13 +726,17 @@ void wgrad_bf16_kernel(WgBParams p) {
   // per-thread staging plan (fixed across tiles; TH, TW even so the upsample's floor
   // shift splits over tile origin + offset): gz element k -> (pixel offset, image),
   // halo element k -> packed (image, hy, hx, channel vector) or -1
-  int gzrel[NGZ], gznb[NGZ], hpk[NH];
+  constexpr bool gz_bits = GZB;   // gz = up2(g) * lrelu'(bits) (PG_CONV_GZ_BITS)
+  const int gH = gz_bits ? p.H >> 1 : p.H, gW = gz_bits ? p.W >> 1 : p.W;
+  int gzrel[NGZ], gznb[NGZ], hpk[NH], gbrel[NGZ];
 #pragma unroll
   for (int k = 0; k < NGZ; ++k) {
     const int i = tid + k * 256;
     const int pm = i / GV, v = i - pm * GV;
     const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
-    gzrel[k] = ((nb * p.H + ty) * p.W + tx) * p.gz_cs + 8 * v;
+    const int gs = gz_bits ? 1 : 0;
+    gzrel[k] = ((nb * gH + (ty >> gs)) * gW + (tx >> gs)) * p.gz_cs + 8 * v;
+    gbrel[k] = ((nb * p.H + ty) * p.W + tx) * p.gzb_cs + ((o0 + 8 * v) >> 3);
     gznb[k] = (o0 + 8 * v < p.cout) ? nb : 1 << 20;
   }
 #pragma unroll
@@ -739,16 +750,23 @@ void wgrad_bf16_kernel(WgBParams p) {
       if (c0 + 8 * v < p.x_cs) hpk[k] = (nb << 24) | (hy << 16) | (hx << 8) | v;
     }
   }
-  auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH]) {
+  auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH], int (&rb)[NGZ]) {
     const int tx0 = (t % p.tiles_x) * p.TW;
     int tt = t / p.tiles_x;
     const int ty0 = (tt % p.tiles_y) * p.TH;
     const int b0 = (tt / p.tiles_y) * p.NB;
-    const bf16_t* gzt = p.gz + (((size_t)b0 * p.H + ty0) * p.W + tx0) * p.gz_cs + o0;
+    const int gs = gz_bits ? 1 : 0;
+    const bf16_t* gzt = p.gz + (((size_t)b0 * gH + (ty0 >> gs)) * gW + (tx0 >> gs)) * p.gz_cs + o0;
+    const unsigned char* gbt =
+        gz_bits ? p.gzb + (((size_t)b0 * p.H + ty0) * p.W + tx0) * p.gzb_cs : nullptr;
 #pragma unroll
     for (int k = 0; k < NGZ; ++k) {
       rg[k] = u32x4_t{0u, 0u, 0u, 0u};
-      if (b0 + gznb[k] < p.B) rg[k] = *reinterpret_cast<const u32x4_t*>(gzt + gzrel[k]);
+      rb[k] = 0xff;
+      if (b0 + gznb[k] < p.B) {
+        rg[k] = *reinterpret_cast<const u32x4_t*>(gzt + gzrel[k]);
+        if (gz_bits) rb[k] = gbt[gbrel[k]];
+      }
     }
     const int ys = p.ups ? 1 : 0;
     const bf16_t* xb = p.x + c0;
@@ -763,17 +781,28 @@ void wgrad_bf16_kernel(WgBParams p) {
             xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff));
     }
   };
-  auto store_tile = [&](const u32x4_t (&rg)[NGZ], const u32x4_t (&rh)[NH]) {
+  auto store_tile = [&](const u32x4_t (&rg0)[NGZ], const u32x4_t (&rh)[NH], const int (&rb)[NGZ]) {
 #pragma unroll
     for (int k = 0; k < NGZ; ++k) {
       const int i = tid + k * 256;
       const int pm = i / GV, v = i - pm * GV;
-      *reinterpret_cast<u32x4_t*>(gzl + grow(pm) + 8 * v) = rg[k];
+      u32x4_t rg = rg0[k];
+      if (gz_bits && rb[k] != 0xff) {   // up2(g) * lrelu'(bits), rounded as the unfused gz
+        const int m = rb[k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = bf_lo(rg[e]), c = bf_hi(rg[e]);
+          if (!((m >> (2 * e)) & 1)) a *= p.slope;
+          if (!((m >> (2 * e + 1)) & 1)) c *= p.slope;
+          rg[e] = pack_bf16x2(a, c);
+        }
+      }
+      *reinterpret_cast<u32x4_t*>(gzl + grow(pm) + 8 * v) = rg;
       if (do_db) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          bs[2 * e] += bf_lo(rg[k][e]);
-          bs[2 * e + 1] += bf_hi(rg[k][e]);
+          bs[2 * e] += bf_lo(rg[e]);
+          bs[2 * e + 1] += bf_hi(rg[e]);
         }
       }
     }
@@ -829,19 +858,20 @@ void wgrad_bf16_kernel(WgBParams p) {
   // PD tiles of global loads in flight: tile t+PD is fetched into the register set that
   // tile t just left, right after it was written to LDS
   u32x4_t rg[PD][NGZ], rh[PD][NH];
+  int rb[PD][NGZ];
   const int t_begin = blockIdx.z * p.tiles_per_split;
   const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
 #pragma unroll
   for (int d = 0; d < PD; ++d)
-    if (t_begin + d < t_end) load_tile(t_begin + d, rg[d], rh[d]);
+    if (t_begin + d < t_end) load_tile(t_begin + d, rg[d], rh[d], rb[d]);
   for (int t = t_begin; t < t_end; t += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
       if (t + d < t_end) {
         __syncthreads();   // the previous tile's fragments have been read
-        store_tile(rg[d], rh[d]);
+        store_tile(rg[d], rh[d], rb[d]);
         __syncthreads();
-        if (t + d + PD < t_end) load_tile(t + d + PD, rg[d], rh[d]);
+        if (t + d + PD < t_end) load_tile(t + d + PD, rg[d], rh[d], rb[d]);
         compute_tile();
       }
     }
@@ -985,10 +1015,10 @@ size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
   return pl.splits > 1 ? pl.splits * pl.slab * sizeof(float) : 0;
 }
 
-template <int MO, int NC, int WMO, int WNC, int PD, int WPE>
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
                       float scale, float* dw, float* db, float* ws, size_t ws_bytes,
-                      hipStream_t st) {
+                      hipStream_t st, const void* gzbits) {
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
   WgBParams p;
   p.x = (const bf16_t*)x; p.gz = (const bf16_t*)gz; p.dw = dw; p.db = db;
@@ -1006,6 +1036,11 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.GZS = BO + (BO > 16 ? 16 : 0);
   p.HS = BC + (BC > 16 ? 16 : 0);
   p.halo_elems = pl.tc.NB * (pl.tc.TH + 2) * (pl.tc.TW + 2);
+  p.gzb = (d->flags & PG_CONV_GZ_BITS) ? reinterpret_cast<const unsigned char*>(gzbits) : nullptr;
+  p.gzb_cs = d->xb_cs;
+  p.slope = d->slope;
+  PG_CHECK_ARG(!p.gzb || (d->xb_cs * 8 >= d->cout && pl.tc.TH % 2 == 0 && pl.tc.TW % 2 == 0),
+               "wgrad_bf16: GZ_BITS needs gzbits with >= cout/8 bytes per pixel");
   PG_CHECK_ARG(p.halo_elems <= WGB_MAXHALO, "wgrad_bf16: halo %d > %d", p.halo_elems, WGB_MAXHALO);
   p.slab = pl.slab;
   p.ws = nullptr;
@@ -1023,11 +1058,11 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE>,
+    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE>), dim3(pl.ot, pl.ct, pl.splits),
+  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   if (p.mode == WG_SLABS) {
@@ -1043,17 +1078,35 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   return PG_OK;
 }
 
+// GZ_BITS variants: the tiles of the discriminator's conv b weight gradient at the levels
+// that keep sign bits (1024^2: cout 32 -> MO 2; 512^2: cout 64, cin 32 -> MO 4, WNC 2)
+constexpr bool wgrad_gzb_ok(int MO, int WNC, int PD, int WPE) {
+  return (MO == 2 && WNC == 1 && PD == 2 && WPE == 2) || (MO == 4 && PD == 4 && WPE == 1) ||
+         (MO == 1 && PD == 2);
+}
+
 int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                        float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st) {
+                        float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st,
+                        const void* gzbits = nullptr) {
+  PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS) || gzbits, "wgrad_bf16: GZ_BITS without gzbits");
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
   const WgbPlan pl = wgrad_bf16_plan(d);
   // (prefetch depth, waves per SIMD); PG_WG_VARIANT="pd,wpe" overrides for tuning runs
   int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   if (const char* e = getenv("PG_WG_VARIANT")) sscanf(e, "%d,%d", &pd, &wpe);
-#define PG_WGB(a, b, c, e, PD, WPE)                                                      \
-  if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e && pd == PD && wpe == WPE)  \
-    return launch_wgrad_bf16<a, b, c, e, PD, WPE>(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
+  const bool gzb = (d->flags & PG_CONV_GZ_BITS) != 0;
+#define PG_WGB(a, b, c, e, PD, WPE)                                                        \
+  if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e && pd == PD && wpe == WPE) {  \
+    if constexpr (wgrad_gzb_ok(a, e, PD, WPE)) {                                           \
+      if (gzb)                                                                             \
+        return launch_wgrad_bf16<a, b, c, e, PD, WPE, true>(d, pl, x, gz, scale, dw, db,   \
+                                                            ws, ws_bytes, st, gzbits);     \
+    }                                                                                      \
+    PG_CHECK_ARG(!gzb, "wgrad_bf16: GZ_BITS not instantiated for this tile");              \
+    return launch_wgrad_bf16<a, b, c, e, PD, WPE, false>(d, pl, x, gz, scale, dw, db, ws,  \
+                                                         ws_bytes, st, gzbits);            \
+  }
   PG_WGB(1, 1, 1, 1, 2, 3)
   PG_WGB(1, 1, 1, 2, 2, 2)
   PG_WGB(2, 1, 1, 1, 2, 2)
@@ -1280,6 +1333,14 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 // Which fused epilogues the kernel the dispatcher picks supports.
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
+  constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
+  if (d->flags & BITS) {
+    if constexpr (sizeof(T) != 2) return false;
+    if (!conv_hr_ok(d) || !conv_hr_mode_ok(d)) return false;
+    if ((d->flags & PG_CONV_PIXNORM) && ((d->cout + 15) & ~15) > conv_hr_bn(d)) return false;
+    return true;
+  }
+  if ((d->flags & PG_CONV_MASK) && (d->flags & PG_CONV_POOL)) return false;
   if (!(d->flags & PG_CONV_PIXNORM)) return true;
   if (d->flags & (PG_CONV_POOL | PG_CONV_MASK | PG_CONV_ACCUM)) return false;
   const int cout_p = (d->cout + 15) & ~15;
@@ -1295,11 +1356,12 @@ bool conv_supported(const pg_conv_desc* d, size_t wsb) {
 
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
-                  const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st) {
+                  const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st,
+                  const void* xbits = nullptr) {
   PG_CHECK_ARG(conv_supported<T>(d, wsb), "conv3x3_fwd: flags 0x%x not supported for cout %d at %dx%d",
                d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
-    if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, st);
+    if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, xbits, st);
   }
   int BM, BN;
   conv_tile_for(d->cout, &BM, &BN, d->W);
@@ -1376,16 +1438,30 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
                cinp_of(d->cin));
   PG_CHECK_ARG(d->y_cs >= d->cout && d->y_cs % 4 == 0, "conv3x3_fwd: bad y channel stride");
   PG_CHECK_ARG(!(d->flags & PG_CONV_BIAS) || bias, "conv3x3_fwd: BIAS flag without bias");
-  PG_CHECK_ARG(!(d->flags & PG_CONV_MASK) || (aux && d->aux_cs >= d->cout),
+  PG_CHECK_ARG(!(d->flags & PG_CONV_MASK) ||
+                   (aux && (d->flags & PG_CONV_AUX_BITS ? d->aux_cs * 8 >= d->cout
+                                                         : d->aux_cs >= d->cout)),
                "conv3x3_fwd: MASK flag without aux");
-  PG_CHECK_ARG(!((d->flags & PG_CONV_MASK) && (d->flags & PG_CONV_POOL)),
-               "conv3x3_fwd: MASK and POOL together are not supported");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_Y2_BITS) || (y2 && d->y2_cs * 8 >= d->cout && d->y2_cs % 2 == 0),
+               "conv3x3_fwd: Y2_BITS needs y2 with >= cout/8 bytes per pixel");
   PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM)),
                "conv3x3_fwd: y2 only with POOL or PIXNORM");
   PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_X_BITS), "conv3x3_fwd: X_BITS needs pg_conv3x3_fwd_ex");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
   return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
+}
+
+int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
+                      const void* wpk, const float* bias, const void* aux, void* y, void* y2,
+                      void* ws, size_t ws_bytes, void* stream) {
+  if (!d || !(d->flags & PG_CONV_X_BITS))
+    return pg_conv3x3_fwd(dtype, d, x, wpk, bias, aux, y, y2, ws, ws_bytes, stream);
+  PG_CHECK_ARG(xbits && dtype == PG_BF16, "conv3x3_fwd_ex: X_BITS needs xbits (bf16)");
+  PG_CHECK_ARG(x && wpk && y && d->cout % 4 == 0 && d->x_cs % 8 == 0 && d->y_cs >= d->cout,
+               "conv3x3_fwd_ex: bad args");
+  return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, (hipStream_t)stream, xbits);
 }
 
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes) {
@@ -1402,6 +1478,7 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
                      float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS), "conv3x3_wgrad: GZ_BITS needs pg_conv3x3_wgrad_ex");
   if (dtype == PG_BF16)
     return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream);
   TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
@@ -1432,6 +1509,18 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
     hipLaunchKernelGGL(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   return PG_OK;
+}
+
+int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const void* gz,
+                        const void* gzbits, float scale, float* dw, float* db, void* ws,
+                        size_t ws_bytes, void* stream) {
+  if (!d || !(d->flags & PG_CONV_GZ_BITS))
+    return pg_conv3x3_wgrad(dtype, d, x, gz, scale, dw, db, ws, ws_bytes, stream);
+  PG_CHECK_ARG(x && gz && gzbits && dw && dtype == PG_BF16, "conv3x3_wgrad_ex: GZ_BITS needs gzbits (bf16)");
+  PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4 && d->H % 2 == 0 && d->W % 2 == 0,
+               "conv3x3_wgrad_ex: bad spatial size");
+  return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream,
+                             gzbits);
 }
 
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,

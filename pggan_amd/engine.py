@@ -171,6 +171,8 @@ class StepEngine:
         self.mcs = cinp(d[0] + 1)
         self.keep_fake_D = False
         self.fuse_pixnorm = True   # PixelNorm in the G conv epilogues where the kernel allows
+        self.fuse_dbits = True     # D conv+lrelu+pool outputs kept as sign bits (see _dbits)
+        self.dbits_min_res = 512
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
         self._alloc()
@@ -218,6 +220,9 @@ class StepEngine:
             D["tblend"] = t(B, R // 2, R // 2, d[s - 1])
         for i in range(s):
             Ri = 8 * 2 ** i
+            # lrelu sign bits of the pre-pool conv-b output (used instead of bf{i} where the
+            # kernels support it, see _dbits)
+            D[f"mb{i}"] = torch.zeros(B, Ri, Ri, (d[i] + 7) // 8, dtype=torch.uint8, device=self.dev)
             D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
             D[f"bf{i}"] = t(B, Ri, Ri, d[i])
             D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
@@ -313,15 +318,16 @@ class StepEngine:
 
     # ------------------------------------------------------------------ conv helpers
     def _conv(self, net, key, x, y, H, cin, cout, flags, aux=None, y2=None, out_scale=1.0,
-              dgrad=False, bias=True):
+              dgrad=False, bias=True, xbits=None):
         pf, pd, bs, _ = self.packs[(net, key)]
         if not dgrad and bias:
             flags |= L.CONV_BIAS
         need = self._ws_need("c", H, cin, cout, False)
+        kw = dict(xbits=xbits) if xbits is not None else {}
         self.ops.conv3x3(x, pd if dgrad else pf, y, B=self.B, H=H, W=H, cin=cin, cout=cout,
                          flags=flags, slope=SLOPE, out_scale=out_scale,
                          bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2,
-                         ws=self.ws if need else None)
+                         ws=self.ws if need else None, **kw)
 
     def _ws_need(self, kind, H, cin, cout, ups):
         """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape); the
@@ -339,11 +345,39 @@ class StepEngine:
             self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         return need
 
-    def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None):
+    def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None, gzbits=None,
+               gscale=1.0):
+        """gzbits: gz is the pooled-resolution gradient g and the conv's output gradient is
+        gscale * up2(g) * lrelu'(gzbits) (never materialised)."""
         c = self.packs[(net, key)][3]
         need = self._ws_need("w", H, cin, cout, ups)
-        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=c,
-                            db=db, ws=self.ws if need else None)
+        kw = dict(gzbits=gzbits, slope=SLOPE) if gzbits is not None else {}
+        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
+                            scale=c * gscale, db=db, ws=self.ws if need else None, **kw)
+
+    def _dbits(self, i):
+        """Whether D level i keeps its conv-b (conv + lrelu + pool) output as sign bits only:
+        the forward writes bits instead of the full-resolution activation, and every consumer
+        of its lrelu' mask (input-gradient conv, weight gradient, R1 tangent) reads the bits
+        and the pooled-resolution gradient directly (no unpool_mask pass)."""
+        key = ("dbits", i, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            d, Ri = self.depths, 8 * 2 ** i
+            # below 512^2 the saved bytes no longer pay for the masking work in the staging
+            ok = bool(self.fuse_dbits and f is not None and d[i] % 16 == 0 and
+                      Ri >= self.dbits_min_res)
+            if ok:
+                B = self.B
+                ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
+                        flags=L.CONV_BIAS | L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i], cout=d[i + 1],
+                            flags=L.CONV_UPS_IN | L.CONV_X_BITS | L.CONV_MASK)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
+                            flags=L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_POOL)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i], flags=L.CONV_GZ_BITS))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
 
     def _pn_fused(self, H, cin, cout, flags):
         """Whether this generator conv can run PixelNorm in its epilogue (all output
@@ -464,8 +498,13 @@ class StepEngine:
         for i in reversed(range(s)):                                           # :260-265
             Ri = 8 * 2 ** i
             self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
-            self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
-                       L.CONV_LRELU | L.CONV_POOL, y2=D[f"bf{i}"], out_scale=0.25)
+            if self._dbits(i):
+                self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS, y2=D[f"mb{i}"],
+                           out_scale=0.25)
+            else:
+                self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_LRELU | L.CONV_POOL, y2=D[f"bf{i}"], out_scale=0.25)
             if i == s - 1:
                 ops.blend(1.0 - alpha, D["yd"], alpha, D[f"p{i}"], D["hblend"])
                 h = D["hblend"]
@@ -515,14 +554,22 @@ class StepEngine:
                 ops.unpool_mask(g, D["yd"], D["gzd"], B=B, H=Ri // 2, W=Ri // 2, C=d[i],
                                 scale=1.0 - alpha, slope=SLOPE, ups=False)
             sc = 0.25 * (alpha if i == s - 1 else 1.0)
-            ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
-                            slope=SLOPE, ups=True)
-            if GR is not None:
-                self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
-                            d[i],
-                            db=GR[b + "bias"])
-            self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_MASK,
-                       aux=D[f"a{i}"], dgrad=True)
+            if self._dbits(i):
+                # gzb = sc * up2(g) * lrelu'(bits): read by the kernels from g and the bits
+                if GR is not None:
+                    self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
+                                db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc)
+                self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
+                           L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
+                           dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
+            else:
+                ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
+                                slope=SLOPE, ups=True)
+                if GR is not None:
+                    self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
+                                d[i + 1], d[i], db=GR[b + "bias"])
+                self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
+                           L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
             hin = D["yrgb"] if i == s - 1 else (D["hblend"] if i == s - 2 else D[f"p{i + 1}"])
             if GR is not None:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
@@ -576,11 +623,21 @@ class StepEngine:
             self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
                        aux=D[f"a{i}"], bias=False)
             self._wgrad("D", f"a{i}", t, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1], d[i + 1])
-            self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tbf{i}"], Ri, d[i + 1], d[i], L.CONV_MASK,
-                       aux=D[f"bf{i}"], bias=False)
-            self._wgrad("D", f"b{i}", D[f"ta{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
-                        d[i])
-            ops.avgpool2(D[f"tbf{i}"], D[f"tp{i}"], B=B, H=Ri, W=Ri, C=d[i])
+            if self._dbits(i):
+                # tangent through conv b, lrelu' (bits) and the avg pool in one launch; the
+                # weight term pairs the tangent with B1's gradient at this level
+                self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tp{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_POOL, aux=D[f"mb{i}"],
+                           bias=False, out_scale=0.25)
+                gb1 = D["gh"] if i == 0 else D[f"ghin{i - 1}"]
+                self._wgrad("D", f"b{i}", D[f"ta{i}"], gb1, GR[b + "weight"], Ri, d[i + 1], d[i],
+                            gzbits=D[f"mb{i}"], gscale=0.25 * (alpha if i == s - 1 else 1.0))
+            else:
+                self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tbf{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_MASK, aux=D[f"bf{i}"], bias=False)
+                self._wgrad("D", f"b{i}", D[f"ta{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
+                            d[i + 1], d[i])
+                ops.avgpool2(D[f"tbf{i}"], D[f"tp{i}"], B=B, H=Ri, W=Ri, C=d[i])
             if i == s - 1:
                 ops.blend(1.0 - alpha, D["td"], alpha, D[f"tp{i}"], D["tblend"])
                 t = D["tblend"]

@@ -16,6 +16,27 @@ import torch.nn.functional as F
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
 CONV_PIXNORM = 64
+CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
+FUSED_FLAGS = CONV_PIXNORM | CONV_Y2_BITS | CONV_AUX_BITS | CONV_X_BITS | CONV_GZ_BITS
+
+
+def packbits(m):
+    """bool [..., C] -> uint8 [..., C/8]; channel c at byte c//8, bit c%8 (include/pggan_hip.h)"""
+    m = m.to(torch.uint8).reshape(m.shape[:-1] + (m.shape[-1] // 8, 8))
+    w = torch.tensor([1 << k for k in range(8)], dtype=torch.uint8)
+    return (m * w).sum(-1).to(torch.uint8)
+
+
+def unpackbits(b, C):
+    """uint8 [..., nbytes] -> bool [..., C]"""
+    k = torch.arange(8, dtype=torch.uint8)
+    bits = (b.unsqueeze(-1) >> k) & 1
+    return bits.reshape(b.shape[:-1] + (-1,))[..., :C].bool()
+
+
+def bmask(bits, C, slope):
+    m = unpackbits(bits, C)
+    return torch.where(m, torch.ones(m.shape), torch.full(m.shape, slope))
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW = 1, 2, 4, 8, 16
 
 
@@ -60,7 +81,7 @@ class CpuOps:
         self.fused = fused          # report the fused conv epilogues as supported
 
     def conv_supported(self, *, B, H, W, cin, cout, flags, ws_bytes=0):
-        return self.fused or not (flags & CONV_PIXNORM)
+        return self.fused or not (flags & FUSED_FLAGS)
 
     # -- conv ------------------------------------------------------------
     def packed_elems(self, mode, cout, cin):
@@ -83,12 +104,14 @@ class CpuOps:
         return 0
 
     def conv3x3(self, x, wpk, y, *, B, H, W, cin, cout, flags, slope=0.2, out_scale=1.0,
-                bias=None, aux=None, y2=None, ws=None):
+                bias=None, aux=None, y2=None, ws=None, xbits=None):
         ci, co = cinp(cin), r16(cout)
         Wt = wpk.view(co, 9, ci).permute(0, 2, 1).reshape(co, ci, 3, 3)[:cout]
         xin = nchw(x, ci)
         if flags & CONV_UPS_IN:
             xin = up2(xin)
+        if flags & CONV_X_BITS:
+            xin = xin * bmask(xbits, ci, slope).permute(0, 3, 1, 2)
         z = F.conv2d(xin, Wt, padding=1)
         if flags & CONV_BIAS:
             z = z + bias.view(1, -1, 1, 1)
@@ -101,12 +124,18 @@ class CpuOps:
             if y2 is not None:
                 y2.view(B, H, W)[...] = r[..., 0]
         if flags & CONV_POOL:
+            if (flags & CONV_MASK) and (flags & CONV_AUX_BITS):   # mask before the pool
+                z = z * bmask(aux, cout, slope)
             if y2 is not None:
-                y2[..., :cout] = z
+                if flags & CONV_Y2_BITS:
+                    y2[...] = 0
+                    y2[..., :(cout + 7) // 8] = packbits(z > 0)
+                else:
+                    y2[..., :cout] = z
             z = F.avg_pool2d(z.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4.0
         z = z * out_scale
-        if flags & CONV_MASK:
-            z = z * lmask(aux[..., :cout], slope)
+        if (flags & CONV_MASK) and not (flags & CONV_POOL):
+            z = z * (bmask(aux, cout, slope) if flags & CONV_AUX_BITS else lmask(aux[..., :cout], slope))
         if flags & CONV_ACCUM:
             y[..., :cout] += z
         else:
@@ -115,11 +144,14 @@ class CpuOps:
     def wgrad_workspace_bytes(self, *, B, H, W, cin, cout, ups=False):
         return 0
 
-    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None):
+    def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None,
+                   gzbits=None, slope=0.2):
         xin = nchw(x, cin)
         if ups:
             xin = up2(xin)
         g = nchw(gz, cout)
+        if gzbits is not None:
+            g = up2(g) * bmask(gzbits, cout, slope).permute(0, 3, 1, 2)
         dw += scale * torch.nn.grad.conv2d_weight(xin, (cout, cin, 3, 3), g, padding=1)
         if db is not None:
             db += scale * g.sum((0, 2, 3))

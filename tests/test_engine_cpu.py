@@ -26,6 +26,8 @@ def build(meta, ops, device="cpu"):
     fpD = E.FlatParams(dsh, E.dead_params("D", s), device,
                        {k: torch.from_numpy(v) for k, v in PD.items()})
     eng = E.StepEngine(ops, depths, s, B, device)
+    if device == "cpu":
+        eng.dbits_min_res = 8      # exercise the sign-bit schedule at the fixture sizes
     eng.bind(fpG, fpD, E.Hyper())
     eng.keep_fake_D = True
     return eng, fpG, fpD
@@ -95,8 +97,10 @@ def run_and_check(meta, z, eng, fpG, fpD, to_dev, tol, ptol, gatol=1e-7):
                 continue
             assert_close(fpG.gviews[k].cpu().numpy(), g.numpy(), tol, f"G grad {k}", atol=gatol)
             for k in fp.names:
-                check_tensor(z, f"{pre}param_{net}/{k}", fp.views[k].cpu().numpy(), ptol,
-                             what=f"{net} param ")
+                # second step: Adam's ~lr*sign(g) first update turns fp32 summation-order
+                # differences of near-zero gradients into O(lr) parameter differences
+                check_tensor(z, f"{pre}param_{net}/{k}", fp.views[k].cpu().numpy(),
+                             ptol if t == 0 else max(ptol, 1e-5), what=f"{net} param ")
 
 
 @pytest.mark.parametrize("name", NAMES)

@@ -47,10 +47,10 @@ def _run(s, B, alpha, fuse):
                 gG={k: v.clone() for k, v in fpG.gviews.items() if k not in fpG.dead})
 
 
-FUSIONS = [("fuse_pixnorm", {"fuse_pixnorm": False})]
+FUSIONS = [("fuse_pixnorm", {"fuse_pixnorm": False}), ("fuse_dbits", {"fuse_dbits": False})]
 
 
-@pytest.mark.parametrize("s,B,alpha", [(5, 4, 1.0), (6, 4, 0.5), (7, 4, 1.0)])
+@pytest.mark.parametrize("s,B,alpha", [(5, 4, 1.0), (6, 4, 0.5), (7, 4, 1.0), (8, 2, 0.5)])
 @pytest.mark.parametrize("what,off", FUSIONS)
 def test_fused_matches_unfused_bf16(s, B, alpha, what, off):
     a = _run(s, B, alpha, {})

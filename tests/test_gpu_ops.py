@@ -533,3 +533,62 @@ def test_rgb_vector_shapes(dtype, C, Cp, R):
     for k in res["cpu"]:
         # fp32 weight gradients sum ~1M pixel terms in a different order: 3e-4
         cmp(res["cuda"][k], res["cpu"][k], tol_for(dtype, 3e-4), f"{k} C={C} R={R}")
+
+
+@pytest.mark.parametrize("B,H,c1,c2", [(1, 256, 16, 32), (1, 512, 32, 64), (1, 1024, 16, 32)])
+def test_sign_bit_conv_paths(B, H, c1, c2):
+    """bf16 sign-bit variants of the D conv-b chain (include/pggan_hip.h PG_CONV_*_BITS):
+    forward with Y2_BITS (bits of the pre-pool activation), the R1 tangent with
+    AUX_BITS|MASK|POOL, the input gradient with X_BITS|UPS_IN|MASK and the weight gradient
+    with GZ_BITS, each against the CPU double on the same bf16 data; the bits themselves
+    must match exactly where the activation is not within rounding of 0."""
+    from cpu_ops import (CONV_AUX_BITS, CONV_BIAS, CONV_GZ_BITS, CONV_LRELU, CONV_MASK,
+                         CONV_POOL, CONV_UPS_IN, CONV_X_BITS, CONV_Y2_BITS)
+    hip, cpu = ops_pair(torch.bfloat16)
+    dt = torch.bfloat16
+    for fl, ci, co in ((CONV_BIAS | CONV_LRELU | CONV_POOL | CONV_Y2_BITS, c1, c2),
+                       (CONV_MASK | CONV_AUX_BITS | CONV_POOL, c1, c2),
+                       (CONV_MASK | CONV_UPS_IN | CONV_X_BITS, c2, c1)):
+        assert hip.conv_supported(B=B, H=H, W=H, cin=ci, cout=co, flags=fl), (fl, ci, co)
+    a = q(rnd(B, H, H, c1, seed=81), dt)                    # conv-b input (cin = c1)
+    wf = q(rnd(r16(c2) * 9 * cinp(c1), seed=82, scale=0.05), dt)
+    wd = q(rnd(r16(c1) * 9 * cinp(c2), seed=83, scale=0.05), dt)
+    bias = rnd(c2, seed=84, scale=0.1)
+    g = q(rnd(B, H // 2, H // 2, c2, seed=85), dt)           # pooled-resolution gradient
+    amask = q(rnd(B, H, H, c1, seed=86), dt)                 # lrelu' operand of the dgrad
+    res = {}
+    shared_bits = None
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        d_ = dt if dev == "cuda" else torch.float32
+        A, G, AM = a.to(dev).to(d_), g.to(dev).to(d_), amask.to(dev).to(d_)
+        WF, WD, BS = wf.to(dev).to(d_), wd.to(dev).to(d_), bias.to(dev)
+        r = {}
+        p = torch.zeros(B, H // 2, H // 2, c2, dtype=d_, device=dev)
+        bits = torch.zeros(B, H, H, c2 // 8, dtype=torch.uint8, device=dev)
+        ops.conv3x3(A, WF, p, B=B, H=H, W=H, cin=c1, cout=c2,
+                    flags=CONV_BIAS | CONV_LRELU | CONV_POOL | CONV_Y2_BITS, bias=BS, y2=bits,
+                    out_scale=0.25)
+        r["p"], r["bits"] = p, bits.clone()
+        if shared_bits is None:
+            shared_bits = bits.cpu()
+        bits = shared_bits.to(dev)      # consumers: identical bits on both sides
+        tp = torch.zeros_like(p)
+        ops.conv3x3(A, WF, tp, B=B, H=H, W=H, cin=c1, cout=c2,
+                    flags=CONV_MASK | CONV_AUX_BITS | CONV_POOL, aux=bits, out_scale=0.25)
+        r["tp"] = tp
+        gza = torch.zeros(B, H, H, c1, dtype=d_, device=dev)
+        ops.conv3x3(G, WD, gza, B=B, H=H, W=H, cin=c2, cout=c1,
+                    flags=CONV_MASK | CONV_UPS_IN | CONV_X_BITS, aux=AM, xbits=bits,
+                    out_scale=0.25)
+        r["gza"] = gza
+        dw = torch.zeros(c2, c1, 3, 3, device=dev)
+        db = torch.zeros(c2, device=dev)
+        ops.conv_wgrad(A, G, dw, B=B, H=H, W=H, cin=c1, cout=c2, ups=False, scale=0.5, db=db,
+                       gzbits=bits)
+        r["dw"], r["db"] = dw, db
+        res[dev] = r
+    hb, cb = res["cuda"]["bits"].cpu(), res["cpu"]["bits"]
+    diff = (hb ^ cb).count_nonzero().item()
+    assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
+    for k in ("p", "tp", "gza", "dw", "db"):
+        cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
