@@ -202,6 +202,15 @@ int pg_linear_fwd(int dtype, const pg_linear_desc* d, const void* x, const float
  * IN_CHW/F32_IN describe gx, OUT_CHW/F32_OUT describe gy */
 int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
                     const void* aux, void* gx, void* stream);
+/* bf16 split-reduction forms of the two passes above (deterministic: fp32 partials of
+ * weight slices in ws, then a small epilogue kernel); pass 0 = fwd, 1 = dgrad.  A NULL or
+ * too small ws (or the fp32 mode) falls back to pg_linear_fwd / pg_linear_dgrad. */
+size_t pg_linear_workspace_size(int dtype, const pg_linear_desc* d, int pass);
+int pg_linear_fwd_ws(int dtype, const pg_linear_desc* d, const void* x, const float* w,
+                     const float* b, const void* aux, void* y, void* ws, size_t ws_bytes,
+                     void* stream);
+int pg_linear_dgrad_ws(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
+                       const void* aux, void* gx, void* ws, size_t ws_bytes, void* stream);
 /* accumulates dw[n][k] += scale sum_b gy[b][n] x[b][k]; db[n] += scale sum_b gy[b][n] */
 int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const void* gy, float* dw,
                     float* db, void* stream);

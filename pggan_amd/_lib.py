@@ -85,6 +85,11 @@ _SIGS = {
     "pg_linear_fwd": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_linear_dgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
     "pg_linear_wgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_linear_workspace_size": ([_I, ctypes.POINTER(LinearDesc), _I], _SZ),
+    "pg_linear_fwd_ws": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
+                         _I),
+    "pg_linear_dgrad_ws": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
+                           _I),
     "pg_mbstd_fwd": ([_I, _I, _I, _I, _I, _VP, _I, _VP, _VP], _I),
     "pg_mbstd_bwd": ([_I, _I, _I, _I, _I, _VP, _I, _VP, _VP, _VP], _I),
     "pg_mbstd_r1": ([_I, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP], _I),
@@ -318,19 +323,32 @@ class HipOps:
             flags |= LIN_F32_OUT
         return LinearDesc(B, K, N, in_cs, out_cs, flags, scale, slope)
 
+    def _lin_ws(self, d, pass_, device):
+        """fp32 split-reduction workspace of the bf16 linear kernels (grown on demand,
+        reused: launches are stream-ordered)."""
+        need = int(self.lib.pg_linear_workspace_size(self.dt, ctypes.byref(d), pass_))
+        if not need:
+            return None, 0
+        ws = getattr(self, "_linws", None)
+        if ws is None or ws.numel() * 4 < need or ws.device != device:
+            ws = self._linws = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+        return ws, ws.numel() * 4
+
     def linear(self, x, w, b, y, *, B, flags, scale, slope=0.2, aux=None):
         self._cuda(x, w, b, y, aux)
         N, K = w.shape
         d = self._lin(B, K, N, flags, scale, slope, x, y)
-        self._chk(self.lib.pg_linear_fwd(self.dt, ctypes.byref(d), _p(x), _p(w), _p(b), _p(aux),
-                                         _p(y), self._s()), "linear_fwd")
+        ws, wsb = self._lin_ws(d, 0, y.device)
+        self._chk(self.lib.pg_linear_fwd_ws(self.dt, ctypes.byref(d), _p(x), _p(w), _p(b), _p(aux),
+                                            _p(y), _p(ws), wsb, self._s()), "linear_fwd")
 
     def linear_dgrad(self, gy, w, gx, *, B, flags, scale, slope=0.2, aux=None):
         self._cuda(gy, w, gx, aux)
         N, K = w.shape
         d = self._lin(B, K, N, flags, scale, slope, gx, gy)
-        self._chk(self.lib.pg_linear_dgrad(self.dt, ctypes.byref(d), _p(gy), _p(w), _p(aux), _p(gx),
-                                           self._s()), "linear_dgrad")
+        ws, wsb = self._lin_ws(d, 1, gx.device)
+        self._chk(self.lib.pg_linear_dgrad_ws(self.dt, ctypes.byref(d), _p(gy), _p(w), _p(aux),
+                                              _p(gx), _p(ws), wsb, self._s()), "linear_dgrad")
 
     def linear_wgrad(self, x, gy, dw, db, *, B, flags, scale):
         self._cuda(x, gy, dw, db)

@@ -1048,6 +1048,7 @@ __global__ void cast_kernel(size_t n, const A* x, B* y) {
 }
 
 #include "ew.inc"
+#include "lin.inc"
 
 }  // namespace
 
@@ -1417,6 +1418,35 @@ int pg_linear_fwd(int dtype, const pg_linear_desc* d, const void* x, const float
   return PG_OK;
 }
 
+size_t pg_linear_workspace_size(int dtype, const pg_linear_desc* d, int pass) {
+  if (!d || !lin_fast_ok(dtype, d)) return 0;
+  return pass == 0 ? lin_fwd_plan(d).ws_bytes : lin_dgrad_plan(d).ws_bytes;
+}
+
+int pg_linear_fwd_ws(int dtype, const pg_linear_desc* d, const void* x, const float* w,
+                     const float* b, const void* aux, void* y, void* ws, size_t ws_bytes,
+                     void* stream) {
+  PG_CHECK_ARG(d && x && w && y && d->B > 0 && d->K > 0 && d->N > 0, "linear_fwd: bad args");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_BIAS) || b, "linear_fwd: BIAS without bias");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_fwd: MASK without aux");
+  if (!(ws && lin_fast_ok(dtype, d) && ws_bytes >= lin_fwd_plan(d).ws_bytes))
+    return pg_linear_fwd(dtype, d, x, w, b, aux, y, stream);
+  lin_fwd_fast<bf16_t>(d, x, w, b, aux, y, (float*)ws, (hipStream_t)stream);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_linear_dgrad_ws(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
+                       const void* aux, void* gx, void* ws, size_t ws_bytes, void* stream) {
+  PG_CHECK_ARG(d && gy && w && gx, "linear_dgrad: bad args");
+  PG_CHECK_ARG(!(d->flags & PG_LIN_MASK) || aux, "linear_dgrad: MASK without aux");
+  if (!(ws && lin_fast_ok(dtype, d) && ws_bytes >= lin_dgrad_plan(d).ws_bytes))
+    return pg_linear_dgrad(dtype, d, gy, w, aux, gx, stream);
+  lin_dgrad_fast<bf16_t>(d, gy, w, aux, gx, (float*)ws, (hipStream_t)stream);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
 int pg_linear_dgrad(int dtype, const pg_linear_desc* d, const void* gy, const float* w,
                     const void* aux, void* gx, void* stream) {
   PG_CHECK_ARG(d && gy && w && gx, "linear_dgrad: bad args");
@@ -1440,6 +1470,12 @@ int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const voi
   PG_CHECK_ARG(d && x && gy && dw, "linear_wgrad: bad args");
   const size_t n = (size_t)d->N * d->K;
   hipStream_t st = (hipStream_t)stream;
+  if (lin_fast_ok(dtype, d) && ((uintptr_t)dw & 15) == 0) {   // bf16: coalesced dw streaming
+    hipLaunchKernelGGL(lin_wgrad_v<bf16_t>, dim3((d->K + 1023) / 1024, d->N), dim3(256), 0, st, *d, x,
+                       gy, dw, db);
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   DT_DISPATCH(dtype, linear_wgrad_kernel, dim3(grid_for(n)), dim3(256), 0, st, *d, x, gy, dw, db);
   PG_LAUNCH_CHECK();
   return PG_OK;

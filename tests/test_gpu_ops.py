@@ -424,7 +424,7 @@ def test_conv_pack_batch(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B", [4, 11])
+@pytest.mark.parametrize("B", [4, 11, 20])
 def test_linear_paper_sizes(dtype, B):
     """The mbstd linear (K = 16*512 CHW gather -> 512) and the latent layer (512 -> 16*512
     CHW scatter) at the paper width, forward and input gradient."""
