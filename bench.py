@@ -8,7 +8,8 @@ random-init weights (reference init: W ~ N(0,1), b = 0).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
          (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
-One process per GPU; gradients all-reduced (mean) over RCCL before each Adam step.
+One process per GPU; gradients all-reduced (mean) over RCCL before each Adam step, the
+exchange overlapped with the work that does not depend on it (engine.train_step).
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -201,11 +202,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    # PG_DIST_BACKEND=gloo + ranks sharing a GPU: a rehearsal of the N>1 path on a 1-GPU box
+    backend = os.environ.get("PG_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from pggan_amd import _lib
     from pggan_amd import engine as E
@@ -226,10 +234,20 @@ def main():
     real = torch.rand(B, 3, R, R, device=dev, generator=gen) * 2 - 1
     z = torch.empty(2, B, 512, device=dev)
 
+    class Pending:
+        """Async RCCL all-reduce of a net's flat live gradient; the engine waits (and the
+        mean is applied) right before that net's Adam step, so the exchange overlaps the
+        work that does not depend on it (engine.train_step)."""
+
+        def __init__(self, g):
+            self.g, self.work = g, dist.all_reduce(g, async_op=True)
+
+        def wait(self):
+            self.work.wait()
+            self.g.mul_(1.0 / world)
+
     def hook(net, g):
-        if world > 1:
-            dist.all_reduce(g)
-            g.mul_(1.0 / world)
+        return Pending(g) if world > 1 else None
 
     step_no = [0]
 
@@ -240,6 +258,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    eng.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -249,6 +268,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    eng.flush()          # the last step's (deferred) generator update is part of the step
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -261,6 +281,7 @@ def main():
     h0 = time.perf_counter()
     for _ in range(2):
         step()
+    eng.flush()
     host_ms = (time.perf_counter() - h0) * 1e3 / 2
     torch.cuda.synchronize()
     t = torch.tensor([dt], device=dev, dtype=torch.float64)

@@ -297,6 +297,8 @@ class StepEngine:
         launch per net (table of pointers built once, rebuilt if a tensor moves)."""
         if not hasattr(self, "packs"):
             self.alloc_packs()
+        if hasattr(self, "_packed"):
+            self._packed[net] = True
         ops = self.ops
         if hasattr(ops, "pack_table"):
             ents = []
@@ -659,9 +661,10 @@ class StepEngine:
         return D["tout"], D["inj"]
 
     # ================================================================== step
-    def d_step(self, PG, PD, GD, real, z, alpha_G, alpha_D, gp_eps=None):
+    def d_step(self, PG, PD, GD, real, z, alpha_G, alpha_D, gp_eps=None, before_fake=None):
         """D half of train_step (pggan/model.py:211-238).  Returns the faded real image and
-        the fake image.  Gradients are written to GD (zeroed here)."""
+        the fake image.  Gradients are written to GD (zeroed here).  before_fake() runs
+        between the real-image part (which does not read G) and the fake image."""
         ops, D, B, hp = self.ops, self.dd, self.B, self.hyper
         GD_flat = self._GD_flat
         GD_flat.zero_()
@@ -685,6 +688,8 @@ class StepEngine:
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
             self.d_backward(PD, GD, D["u"], alpha_D, img=xr)
+        if before_fake is not None:
+            before_fake()
         # ---- fake
         img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
         if self.keep_fake_D:
@@ -709,12 +714,15 @@ class StepEngine:
         # upstream of the second backward: no BCE here, so no logit injection
         self.d_backward(PD, GD, D["zeros"], alpha, img=D["interp"], inj_mbstd=inj)
 
-    def g_step(self, PG, PD, GG, z, alpha_G, alpha_D):
-        """G half of train_step (pggan/model.py:244-253)."""
+    def g_step(self, PG, PD, GG, z, alpha_G, alpha_D, before_d=None):
+        """G half of train_step (pggan/model.py:244-253).  before_d() runs after the
+        generator forward (which does not read D) and before D is evaluated."""
         ops, D, hp = self.ops, self.dd, self.hyper
         self._GG_flat.zero_()
         self.loss[3:4].zero_()
         img = self.g_forward(PG, z, alpha_G)
+        if before_d is not None:
+            before_d()
         self.d_forward(PD, img, alpha_D)
         ops.bce(D["logit"], True, hp.W_adv, self.loss[3:4], D["u"], None)   # pggan/loss.py:5-14
         D["gimg"].zero_()
@@ -725,6 +733,8 @@ class StepEngine:
     def bind(self, fpG: FlatParams, fpD: FlatParams, hyper: Hyper):
         self.fpG, self.fpD, self.hyper = fpG, fpD, hyper
         self._GD_flat, self._GG_flat = fpD.grad, fpG.grad
+        self._pending_G = None     # deferred Adam_G (overlapped DP mode)
+        self._packed = {"G": False, "D": False}   # packed weights match the parameters
 
     def adam(self, fp: FlatParams, lr):
         hp = self.hyper
@@ -735,19 +745,59 @@ class StepEngine:
 
     def train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
         """One full step: D half (R1) + Adam_D, G half + Adam_G (pggan/model.py:206-255).
-        grad_hook(net, flat_live_grad) runs before each Adam (DP all-reduce)."""
+
+        grad_hook(net, flat_live_grad) runs before each Adam (DP all-reduce).  If it returns
+        an object with .wait() (an async collective, e.g. torch.distributed work), the
+        engine overlaps the exchange with work that does not depend on it:
+          D gradients  -> the G half's generator forward (G is not changed by Adam_D);
+          G gradients  -> the next step's real-image part of the D half (which never
+                          reads G); Adam_G and the G weight packing then run just before
+                          that step's fake image.  flush() completes a pending G update.
+        The arithmetic and its order per parameter are the reference's either way."""
         fpG, fpD, hp = self.fpG, self.fpD, self.hyper
         PG, PD = fpG.views, fpD.views
-        self.pack("G", PG)
-        self.pack("D", PD)
+        if self._pending_G is None and not self._packed["G"]:
+            self.pack("G", PG)
+        if not self._packed["D"]:
+            self.pack("D", PD)
         img_real, img_fake_D = self.d_step(PG, PD, fpD.gviews, real, z1, alpha_G, alpha_D,
-                                           gp_eps=gp_eps)
-        if grad_hook is not None:
-            grad_hook("D", fpD.live_grad())
-        self.adam(fpD, hp.lr_D)
-        self.pack("D", PD)
-        img_fake = self.g_step(PG, PD, fpG.gviews, z2, alpha_G, alpha_D)
-        if grad_hook is not None:
-            grad_hook("G", fpG.live_grad())
-        self.adam(fpG, hp.lr_G)
+                                           gp_eps=gp_eps, before_fake=self._finish_G)
+        hD = grad_hook("D", fpD.live_grad()) if grad_hook is not None else None
+
+        def finish_D():
+            if hD is not None and hasattr(hD, "wait"):
+                hD.wait()
+            self.adam(fpD, hp.lr_D)
+            self.pack("D", PD)
+
+        if hD is not None and hasattr(hD, "wait"):
+            img_fake = self.g_step(PG, PD, fpG.gviews, z2, alpha_G, alpha_D, before_d=finish_D)
+        else:
+            finish_D()
+            img_fake = self.g_step(PG, PD, fpG.gviews, z2, alpha_G, alpha_D)
+        hG = grad_hook("G", fpG.live_grad()) if grad_hook is not None else None
+        self._pending_G = hG if hG is not None else True
+        if not (hG is not None and hasattr(hG, "wait")):
+            self._finish_G()
         return img_real, img_fake_D, img_fake
+
+    def _finish_G(self):
+        """Adam_G (after the pending G all-reduce, if any) and the G weight packing."""
+        h = self._pending_G
+        if h is None:
+            return
+        self._pending_G = None
+        if hasattr(h, "wait"):
+            h.wait()
+        self.adam(self.fpG, self.hyper.lr_G)
+        self.pack("G", self.fpG.views)
+
+    def flush(self):
+        """Complete a deferred G update (overlapped DP mode); no-op otherwise."""
+        self._finish_G()
+
+    def params_changed(self):
+        """Parameters were modified outside the engine (checkpoint load, broadcast):
+        repack both nets at the next step."""
+        self.flush()
+        self._packed = {"G": False, "D": False}

@@ -29,7 +29,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, overlap=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
@@ -49,16 +49,39 @@ def _worker(rank, world, port, out_dir):
         dist.all_reduce(g)
         g.mul_(1.0 / world)
 
+    class Pending:   # bench.py's overlapped form: async all-reduce, mean applied on wait()
+        def __init__(self, g):
+            self.g, self.w = g, dist.all_reduce(g, async_op=True)
+
+        def wait(self):
+            self.w.wait()
+            self.g.mul_(1.0 / world)
+
     eng.train_step(torch.from_numpy(st["real"]), torch.from_numpy(st["z1"]),
-                   torch.from_numpy(st["z2"]), ALPHA, ALPHA, grad_hook=hook)
+                   torch.from_numpy(st["z2"]), ALPHA, ALPHA,
+                   grad_hook=(lambda net, g: Pending(g)) if overlap else hook)
+    eng.flush()
+    gD1, gG1 = fpD.grad.clone(), fpG.grad.clone()
+    # a second step (the deferred G update of step 1 lands inside it in overlap mode)
+    st2 = make_inputs(B, 4 * 2 ** S, seed=700 + rank)[0]
+    eng.train_step(torch.from_numpy(st2["real"]), torch.from_numpy(st2["z1"]),
+                   torch.from_numpy(st2["z2"]), ALPHA, ALPHA,
+                   grad_hook=(lambda net, g: Pending(g)) if overlap else hook)
+    eng.flush()
+    np.savez(os.path.join(out_dir, f"rank{rank}_2.npz"), pD=fpD.flat.numpy(), pG=fpG.flat.numpy())
+    fpD.grad.copy_(gD1)
+    fpG.grad.copy_(gG1)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), gD=fpD.grad.numpy(),
              gG=fpG.grad.numpy(), pD=fpD.flat.numpy(), pG=fpG.flat.numpy())
     dist.destroy_process_group()
 
 
-def test_dp_gradients_are_mean_of_shard_gradients(tmp_path):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_gradients_are_mean_of_shard_gradients(tmp_path, overlap):
+    """overlap: the async all-reduce schedule (D exchange beside the G forward, G exchange
+    deferred into the next step) must give the same result."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), overlap), nprocs=world, join=True)
     r = [np.load(tmp_path / f"rank{i}.npz") for i in range(world)]
     # identical after the all-reduce and both Adam steps
     for k in ("gD", "gG", "pD", "pG"):
@@ -83,3 +106,17 @@ def test_dp_gradients_are_mean_of_shard_gradients(tmp_path):
     n = fpD.n_live
     err = np.linalg.norm(r[0]["gD"][:n] - ref[:n]) / np.linalg.norm(ref[:n])
     assert err < 1e-4, err
+
+
+def test_dp_overlap_is_bitwise_identical(tmp_path):
+    """Two steps with the overlapped schedule == two steps with the synchronous one."""
+    world = 2
+    out = {}
+    for ov in (False, True):
+        d = tmp_path / f"ov{int(ov)}"
+        d.mkdir()
+        mp.spawn(_worker, args=(world, _free_port(), str(d), ov), nprocs=world, join=True)
+        out[ov] = [np.load(d / f"rank{i}_2.npz") for i in range(world)]
+    for i in range(world):
+        for k in ("pD", "pG"):
+            assert np.array_equal(out[False][i][k], out[True][i][k]), (i, k)
