@@ -45,6 +45,7 @@ struct ConvParams {
   // PG_CONV_X_BITS: sign bits masking the input on load ([B][H][W][xb_cs bytes], conv res)
   const unsigned char* xbits;
   int xb_cs;
+  int lg_tx, lg_ty;   // conv_hr: log2 of the tile counts along x and y
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
@@ -176,11 +177,10 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   auto prefetch = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < MAXV; ++j) {
-      buf[j] = u32x4_t{0u, 0u, 0u, 0u};
-      if (soff[j] >= 0) {
-        const T* base = ((wmask >> j) & 1u) ? wsrc : xs;
-        buf[j] = *reinterpret_cast<const u32x4_t*>(base + soff[j] + c0);
-      }
+      // branch-free (clamped address; the zero fill is applied at the LDS write): a load
+      // under a per-lane branch, or a select right after it, makes hipcc wait for it
+      const T* base = ((wmask >> j) & 1u) ? wsrc : xs;
+      buf[j] = *reinterpret_cast<const u32x4_t*>(base + (soff[j] >= 0 ? soff[j] + c0 : 0));
     }
   };
 
@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < MAXV; ++j)
-      if (loff[j] >= 0) *reinterpret_cast<u32x4_t*>(smem + loff[j]) = buf[j];
+      if (loff[j] >= 0)
+        *reinterpret_cast<u32x4_t*>(smem + loff[j]) = soff[j] >= 0 ? buf[j] : u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
     if (ch + 1 < ch_end) prefetch((ch + 1) * p.CK);
     for (int ks = 0; ks < p.KS; ++ks) {
@@ -750,44 +751,52 @@ void wgrad_bf16_kernel(WgBParams p) {
       if (c0 + 8 * v < p.x_cs) hpk[k] = (nb << 24) | (hy << 16) | (hx << 8) | v;
     }
   }
-  auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH], int (&rb)[NGZ]) {
+  // ok masks of a loaded tile: bit k of gz vector k / halo vector k (zero fill at the
+  // LDS write, so the loaded registers are not touched before then)
+  auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH], int (&rb)[NGZ],
+                       unsigned& gok, unsigned& hok) {
     const int tx0 = (t % p.tiles_x) * p.TW;
     int tt = t / p.tiles_x;
     const int ty0 = (tt % p.tiles_y) * p.TH;
     const int b0 = (tt / p.tiles_y) * p.NB;
     const int gs = gz_bits ? 1 : 0;
+    gok = 0;
+    hok = 0;
     const bf16_t* gzt = p.gz + (((size_t)b0 * gH + (ty0 >> gs)) * gW + (tx0 >> gs)) * p.gz_cs + o0;
     const unsigned char* gbt =
         gz_bits ? p.gzb + (((size_t)b0 * p.H + ty0) * p.W + tx0) * p.gzb_cs : nullptr;
 #pragma unroll
     for (int k = 0; k < NGZ; ++k) {
-      rg[k] = u32x4_t{0u, 0u, 0u, 0u};
-      rb[k] = 0xff;
-      if (b0 + gznb[k] < p.B) {
-        rg[k] = *reinterpret_cast<const u32x4_t*>(gzt + gzrel[k]);
-        if (gz_bits) rb[k] = gbt[gbrel[k]];
-      }
+      // branch-free, as in conv_hr's fetch_halo: clamped address, zero fill at the LDS write
+      const bool ok = b0 + gznb[k] < p.B;
+      rg[k] = *reinterpret_cast<const u32x4_t*>(ok ? gzt + gzrel[k] : p.gz);
+      if constexpr (gz_bits) rb[k] = *(ok ? gbt + gbrel[k] : p.gzb);
+      gok |= (ok ? 1u : 0u) << k;
     }
     const int ys = p.ups ? 1 : 0;
     const bf16_t* xb = p.x + c0;
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
-      rh[k] = u32x4_t{0u, 0u, 0u, 0u};
       const int pk = hpk[k];
       const int b = b0 + (pk >> 24), yy = ty0 + ((pk >> 16) & 0xff) - 1,
                 xx = tx0 + ((pk >> 8) & 0xff) - 1;
-      if (pk >= 0 && b < p.B && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
-        rh[k] = *reinterpret_cast<const u32x4_t*>(
-            xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff));
+      const bool ok =
+          pk >= 0 && b < p.B && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      rh[k] = *reinterpret_cast<const u32x4_t*>(
+          ok ? xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff)
+             : p.x);
+      hok |= (ok ? 1u : 0u) << k;
     }
   };
-  auto store_tile = [&](const u32x4_t (&rg0)[NGZ], const u32x4_t (&rh)[NH], const int (&rb)[NGZ]) {
+  auto store_tile = [&](const u32x4_t (&rg0)[NGZ], const u32x4_t (&rh)[NH], const int (&rb)[NGZ],
+                        unsigned gok, unsigned hok) {
 #pragma unroll
     for (int k = 0; k < NGZ; ++k) {
       const int i = tid + k * 256;
       const int pm = i / GV, v = i - pm * GV;
-      u32x4_t rg = rg0[k];
-      if (gz_bits && rb[k] != 0xff) {   // up2(g) * lrelu'(bits), rounded as the unfused gz
+      const bool ok = (gok >> k) & 1u;
+      u32x4_t rg = ok ? rg0[k] : u32x4_t{0u, 0u, 0u, 0u};
+      if (gz_bits && ok && rb[k] != 0xff) {   // up2(g) * lrelu'(bits), rounded as the unfused gz
         const int m = rb[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -811,7 +820,8 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int i = tid + k * 256;
       if (i < nhalo) {
         const int hp = i / HV, v = i - hp * HV;
-        *reinterpret_cast<u32x4_t*>(hal + hrow(hp) + 8 * v) = rh[k];
+        *reinterpret_cast<u32x4_t*>(hal + hrow(hp) + 8 * v) =
+            ((hok >> k) & 1u) ? rh[k] : u32x4_t{0u, 0u, 0u, 0u};
       }
     }
   };
@@ -859,19 +869,21 @@ void wgrad_bf16_kernel(WgBParams p) {
   // tile t just left, right after it was written to LDS
   u32x4_t rg[PD][NGZ], rh[PD][NH];
   int rb[PD][NGZ];
+  unsigned gokr[PD], hokr[PD];
   const int t_begin = blockIdx.z * p.tiles_per_split;
   const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
+  // tiles past the end re-load the last tile (never stored): no branch around the loads
 #pragma unroll
   for (int d = 0; d < PD; ++d)
-    if (t_begin + d < t_end) load_tile(t_begin + d, rg[d], rh[d], rb[d]);
+    load_tile(min(t_begin + d, t_end - 1), rg[d], rh[d], rb[d], gokr[d], hokr[d]);
   for (int t = t_begin; t < t_end; t += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
       if (t + d < t_end) {
         __syncthreads();   // the previous tile's fragments have been read
-        store_tile(rg[d], rh[d], rb[d]);
+        store_tile(rg[d], rh[d], rb[d], gokr[d], hokr[d]);
         __syncthreads();
-        if (t + d + PD < t_end) load_tile(t + d + PD, rg[d], rh[d], rb[d]);
+        load_tile(min(t + d + PD, t_end - 1), rg[d], rh[d], rb[d], gokr[d], hokr[d]);
         compute_tile();
       }
     }
