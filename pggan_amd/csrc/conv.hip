@@ -95,8 +95,21 @@ struct Frag<float> {
   }
 };
 
-template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR>
+// CKC > 0: the channel chunk is fixed at compile time (CKC == p.CK), so the k-step loop
+// unrolls and each k-step's tap / channel offset is a constant (the 4x4..64x64 convs at
+// 256-512 channels are otherwise bound by that per-k-step index arithmetic)
+template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR, int CKC = 0, int TWC = 0,
+          int THC = 0>
 __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
+  // geometry: compile-time where the launch fixes it (TWC/THC/CKC > 0), else from p
+  constexpr int SZ = (int)sizeof(T);
+  const int cTW = TWC > 0 ? TWC : p.TW, cTH = THC > 0 ? THC : p.TH;
+  const int cNB = TWC > 0 ? BM / (TWC * THC) : p.NB;
+  const int cCK = CKC > 0 ? CKC : p.CK;
+  const int cKS = CKC > 0 ? (9 * CKC + 31) / 32 : p.KS;
+  const int cpixb = CKC > 0 ? CKC * SZ + (CKC * SZ >= 64 ? (SZ == 2 ? 32 : 16) : 0) : p.pixb;
+  const int cwrowb = CKC > 0 ? cKS * 32 * SZ + (SZ == 2 ? 32 : 16) : p.wrowb;
+  const int chalo = (CKC > 0 && TWC > 0) ? ((cNB * (cTH + 2) * (cTW + 2) * cpixb + 15) & ~15) : p.halo_bytes;
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
   static_assert(WM * WN == 4, "4 waves");
@@ -106,25 +119,25 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const int g = lane >> 4, r = lane & 15;
 
   int t = blockIdx.x;
-  const int tx0 = (t % p.tiles_x) * p.TW;
+  const int tx0 = (t % p.tiles_x) * cTW;
   t /= p.tiles_x;
-  const int ty0 = (t % p.tiles_y) * p.TH;
+  const int ty0 = (t % p.tiles_y) * cTH;
   t /= p.tiles_y;
-  const int b0 = t * p.NB;
+  const int b0 = t * cNB;
   const int n0 = blockIdx.y * BN;
 
-  const int TW2 = p.TW + 2;
-  const int HW2 = (p.TH + 2) * TW2;
-  const int npix_halo = p.NB * HW2;
+  const int TW2 = cTW + 2;
+  const int HW2 = (cTH + 2) * TW2;
+  const int npix_halo = cNB * HW2;
   char* halo = smem;
-  char* wl = smem + p.halo_bytes;
+  char* wl = smem + chalo;
 
   int hoff[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int pm = wm * (BM / WM) + mt * 16 + r;
-    const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
-    hoff[mt] = ((nb * (p.TH + 2) + ty) * TW2 + tx) * p.pixb;
+    const int tx = pm % cTW, ty = (pm / cTW) % cTH, nb = pm / (cTW * cTH);
+    hoff[mt] = ((nb * (cTH + 2) + ty) * TW2 + tx) * cpixb;
   }
 
   f32x4_t acc[MT][NT];
@@ -134,8 +147,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const bool ups = (p.flags & PG_CONV_UPS_IN) != 0;
-  const int vpp = p.CK * (int)sizeof(T) / 16;  // 16-byte vectors per halo pixel / per tap
-  const int ntap_pad = p.KS * 32 / p.CK;
+  const int vpp = cCK * (int)sizeof(T) / 16;  // 16-byte vectors per halo pixel / per tap
+  const int ntap_pad = cKS * 32 / cCK;
   constexpr int EPV = 16 / (int)sizeof(T);     // elements per 16-byte vector
 
   // Staging plan, computed once: this thread's 16-byte vectors of the halo tile and of
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       const int nb = hp / HW2, rem = hp - nb * HW2;
       const int hy = rem / TW2, hx = rem - hy * TW2;
       const int b = b0 + nb, yy = ty0 + hy - 1, xx = tx0 + hx - 1;
-      loff[j] = hp * p.pixb + v * 16;
+      loff[j] = hp * cpixb + v * 16;
       if (b < p.B && yy >= 0 && yy < p.H && xx >= 0 && xx < p.W) {
         const int sy = ups ? (yy >> 1) : yy, sx = ups ? (xx >> 1) : xx;
         soff[j] = (int)((((size_t)b * p.Hin + sy) * p.Win + sx) * p.x_cs + v * EPV);
@@ -166,7 +179,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       const int row = iw / (ntap_pad * vpp), rem = iw - row * (ntap_pad * vpp);
       const int tap = rem / vpp, v = rem - tap * vpp;
       const int n = n0 + row;
-      loff[j] = p.halo_bytes + row * p.wrowb + tap * p.CK * (int)sizeof(T) + v * 16;
+      loff[j] = chalo + row * cwrowb + tap * cCK * (int)sizeof(T) + v * 16;
       wmask |= 1u << j;
       if (tap < 9 && n < p.cout_p) soff[j] = (n * 9 + tap) * p.cin_p + v * EPV;
     }
@@ -186,7 +199,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
 
   const int ch_begin = blockIdx.z * p.cps;
   const int ch_end = min(p.nchunks, ch_begin + p.cps);
-  if (ch_begin < ch_end) prefetch(ch_begin * p.CK);
+  if (ch_begin < ch_end) prefetch(ch_begin * cCK);
   for (int ch = ch_begin; ch < ch_end; ++ch) {
     __syncthreads();
 #pragma unroll
@@ -194,17 +207,18 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       if (loff[j] >= 0)
         *reinterpret_cast<u32x4_t*>(smem + loff[j]) = soff[j] >= 0 ? buf[j] : u32x4_t{0u, 0u, 0u, 0u};
     __syncthreads();
-    if (ch + 1 < ch_end) prefetch((ch + 1) * p.CK);
-    for (int ks = 0; ks < p.KS; ++ks) {
+    if (ch + 1 < ch_end) prefetch((ch + 1) * cCK);
+    auto kstep = [&](int ks) {
+      const int CKr = cCK;
       const int k0 = ks * 32 + 8 * g;
-      int tap = k0 / p.CK;
-      const int c = k0 - tap * p.CK;
+      int tap = k0 / CKr;
+      const int c = k0 - tap * CKr;
       if (tap > 8) tap = 8;  // padded taps: weights are zero, read real data
-      const int toff = ((tap / 3) * TW2 + (tap % 3)) * p.pixb + c * (int)sizeof(T);
+      const int toff = ((tap / 3) * TW2 + (tap % 3)) * cpixb + c * (int)sizeof(T);
       Frag<T> bfr[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
-        bfr[nt].load(wl + (wn * (BN / WN) + nt * 16 + r) * p.wrowb + k0 * (int)sizeof(T));
+        bfr[nt].load(wl + (wn * (BN / WN) + nt * 16 + r) * cwrowb + k0 * (int)sizeof(T));
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         Frag<T> afr;
@@ -217,6 +231,12 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
             Frag<T>::mma(afr, bfr[nt], acc[mt][nt]);   // D[pixel][cout]
         }
       }
+    };
+    if constexpr (CKC > 0) {
+#pragma unroll
+      for (int ks = 0; ks < (9 * CKC + 31) / 32; ++ks) kstep(ks);
+    } else {
+      for (int ks = 0; ks < cKS; ++ks) kstep(ks);
     }
   }
 
@@ -231,7 +251,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int pm = wm * (BM / WM) + mt * 16 + r;
-        const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+        const int tx = pm % cTW, ty = (pm / cTW) % cTH, nb = pm / (cTW * cTH);
         const int b = b0 + nb;
         const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
         float v[NT][4];
@@ -278,7 +298,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int pm = wm * (BM / WM) + mt * 16 + r;
-        const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+        const int tx = pm % cTW, ty = (pm / cTW) % cTH, nb = pm / (cTW * cTH);
         const int b = b0 + nb;
         const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
         float v[4];
@@ -313,16 +333,16 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
             Ty<T>::st4(dst, v);
           }
         } else {
-          if (p.y2 && b < p.B && nok && !(p.TW >= 16 && (mt & 1)))
+          if (p.y2 && b < p.B && nok && !(cTW >= 16 && (mt & 1)))
             Ty<T>::st4(reinterpret_cast<T*>(p.y2) + pix * p.y2_cs + n, v);
           // 2x2 sum: horizontal partner = lane ^ 1; vertical = lane ^ TW (TW < 16) or the
           // next 16-pixel subtile (TW == 16, handled when mt is the even row)
           float h[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) h[j] = v[j] + __shfl_xor(v[j], 1, 64);
-          if (p.TW < 16) {
+          if (cTW < 16) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) h[j] += __shfl_xor(h[j], p.TW, 64);
+            for (int j = 0; j < 4; ++j) h[j] += __shfl_xor(h[j], cTW, 64);
           } else {
             if (mt & 1) continue;
             if (mt + 1 < MT) {
@@ -392,7 +412,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
       if (n >= p.cout_p) continue;
-      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int tx = pm % cTW, ty = (pm / cTW) % cTH, nb = pm / (cTW * cTH);
       const int b = b0 + nb;
       if (b >= p.B) continue;
       const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
@@ -404,7 +424,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
       if (n >= p.cout) continue;
-      const int tx = pm % p.TW, ty = (pm / p.TW) % p.TH, nb = pm / (p.TW * p.TH);
+      const int tx = pm % cTW, ty = (pm / cTW) % cTH, nb = pm / (cTW * cTH);
       const int b = b0 + nb;
       if (b >= p.B) continue;
       const size_t pix = ((size_t)b * p.H + ty0 + ty) * p.W + tx0 + tx;
@@ -427,7 +447,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       Ty<T>::st4(dst, v);
     }
   } else {
-    const int PTW = p.TW >> 1, PTH = p.TH >> 1;
+    const int PTW = cTW >> 1, PTH = cTH >> 1;
     const int Ho = p.H >> 1, Wo = p.W >> 1;
     T* y2 = reinterpret_cast<T*>(p.y2);
     for (int i = tid; i < (BM / 4) * NV; i += 256) {
@@ -437,12 +457,12 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
       const int ptx = pp % PTW, pty = (pp / PTW) % PTH, nb = pp / (PTW * PTH);
       const int b = b0 + nb;
       if (b >= p.B) continue;
-      const int pm00 = (nb * p.TH + 2 * pty) * p.TW + 2 * ptx;
+      const int pm00 = (nb * cTH + 2 * pty) * cTW + 2 * ptx;
       float v[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         v[q] = ot[pm00 * ORS + cv + q] + ot[(pm00 + 1) * ORS + cv + q] +
-               ot[(pm00 + p.TW) * ORS + cv + q] + ot[(pm00 + p.TW + 1) * ORS + cv + q];
+               ot[(pm00 + cTW) * ORS + cv + q] + ot[(pm00 + cTW + 1) * ORS + cv + q];
       if (y2) {
 #pragma unroll
         for (int dy = 0; dy < 2; ++dy)
@@ -451,7 +471,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
             const size_t fpix = ((size_t)b * p.H + ty0 + 2 * pty + dy) * p.W + tx0 + 2 * ptx + dx;
             float f[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) f[q] = ot[(pm00 + dy * p.TW + dx) * ORS + cv + q];
+            for (int q = 0; q < 4; ++q) f[q] = ot[(pm00 + dy * cTW + dx) * ORS + cv + q];
             Ty<T>::st4(y2 + fpix * p.y2_cs + n, f);
           }
       }
@@ -493,8 +513,21 @@ __global__ void conv_splitk_epilogue(ConvParams p, int splits) {
       const int yy = pool ? 2 * yo + (k >> 1) : yo, xx = pool ? 2 * xo + (k & 1) : xo;
       const size_t pix = ((size_t)b * p.H + yy) * p.W + xx;
       float a[4] = {bsv[0], bsv[1], bsv[2], bsv[3]};
-      for (int z = 0; z < splits; ++z) {
-        const f32x4_t t = *reinterpret_cast<const f32x4_t*>(p.ws + z * p.slab + pix * p.cout_p + c);
+      const float* src = p.ws + pix * p.cout_p + c;
+      int z = 0;
+      // 4 slabs per round: the loads are issued together (one memory latency per round),
+      // the sum stays in slab order
+      for (; z + 4 <= splits; z += 4) {
+        f32x4_t t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = *reinterpret_cast<const f32x4_t*>(src + (z + u) * p.slab);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[q] += t[u][q];
+      }
+      for (; z < splits; ++z) {
+        const f32x4_t t = *reinterpret_cast<const f32x4_t*>(src + z * p.slab);
 #pragma unroll
         for (int q = 0; q < 4; ++q) a[q] += t[q];
       }
@@ -977,7 +1010,15 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t
   if (i >= slab) return;
   const int s0 = blockIdx.y * spb, s1 = min(splits, s0 + spb);
   float s = 0.f;
-  for (int k = s0; k < s1; ++k) s += ws[(size_t)k * slab + i];
+  int k = s0;
+  for (; k + 4 <= s1; k += 4) {   // 4 loads in flight per round, summed in slab order
+    float t[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t[u] = ws[(size_t)(k + u) * slab + i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += t[u];
+  }
+  for (; k < s1; ++k) s += ws[(size_t)k * slab + i];
   float* dst = i < (size_t)nw ? dw + i : (db ? db + (i - nw) : nullptr);
   if (!dst) return;
   if (gridDim.y == 1)
@@ -1252,7 +1293,8 @@ size_t conv_ws_bytes(const pg_conv_desc* d) {
   return (size_t)sp * d->B * d->H * d->W * ((d->cout + 15) & ~15) * sizeof(float);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR>
+template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR, int CKC = 0, int TWC = 0,
+          int THC = 0>
 int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                 const void* aux, void* y, void* y2, void* ws, size_t ws_bytes, hipStream_t st) {
   TileCfg tc = pick_tile(d->H, d->W, BM, BN);
@@ -1284,6 +1326,9 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   const int epi_bytes = TR ? 0 : BM * (BN + 4) * 4;
   const int lds = main_bytes > epi_bytes ? main_bytes : epi_bytes;
   PG_CHECK_ARG(lds <= 160 * 1024, "conv3x3: LDS %d bytes too large", lds);
+  PG_CHECK_ARG(CKC == 0 || CKC == p.CK, "conv3x3: compile-time chunk %d != %d", CKC, p.CK);
+  PG_CHECK_ARG(TWC == 0 || (TWC == tc.TW && THC == tc.TH), "conv3x3: compile-time tile %dx%d != %dx%d",
+               TWC, THC, tc.TW, tc.TH);
   {
     const int vpp = p.CK * (int)sizeof(T) / 16;
     const int ntot = tc.NB * (tc.TH + 2) * (tc.TW + 2) * vpp + BN * (p.KS * 32 / p.CK) * vpp;
@@ -1301,11 +1346,11 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
             splits);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR>,
+    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(256), lds, st, p);
   if (splits > 1) {
     const bool pool = (d->flags & PG_CONV_POOL) != 0;
     const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
@@ -1379,7 +1424,22 @@ int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const f
   conv_tile_for(d->cout, &BM, &BN, d->W);
   // cout >= 64: [pixel][cout] MFMA + LDS-transposed epilogue; cout <= 32: [cout][pixel]
   // MFMA with the direct epilogue (whole pixel rows per store instruction)
-  if (BN == 64) return launch_conv<T, 128, 64, 2, 2, 16, false>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  if (BN == 64) {
+    if constexpr (sizeof(T) == 2) {
+      if (cinp_of(d->cin) % 32 == 0) {   // chunk = 32 channels: compile-time k loop + tile
+        const TileCfg tc = pick_tile(d->H, d->W, 128, 64);
+#define PG_LC(tw, th)                                                                            \
+  if (tc.TW == tw && tc.TH == th)                                                                \
+    return launch_conv<T, 128, 64, 2, 2, 16, false, 32, tw, th>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+        PG_LC(4, 4)
+        PG_LC(8, 8)
+        PG_LC(16, 8)
+#undef PG_LC
+        return launch_conv<T, 128, 64, 2, 2, 16, false, 32>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+      }
+    }
+    return launch_conv<T, 128, 64, 2, 2, 16, false>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+  }
   if (BN == 32) {
     if (BM == 256) return launch_tr<T, 256, 32>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
     return launch_tr<T, 128, 32>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);

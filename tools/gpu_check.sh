@@ -67,6 +67,17 @@ for step in "$@"; do
           > gpurun_out/pmcq.log 2>&1
       rc=$?; echo "pmcq rc=$rc"; tail -n 3 gpurun_out/pmcq.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     listc) ( rocprofv3 -L > gpurun_out/counters.txt 2>&1 ); echo "listc rc=$?" ;;
+    kbl) run kbl 300 python tools/kbench.py c:32:512:512:8 c:32:512:512:6 c:32:512:512:0 \
+           c:64:256:512:22 c:64:512:256:8 c:64:256:256:6 c:16:512:512:6 c:16:512:512:8 \
+           c:8:512:512:6 c:4:512:512:6 c:128:128:256:22 c:128:256:128:8 c:128:128:128:6 \
+           w:32:512:512:0 w:64:256:512:0 w:64:256:256:0 w:16:512:512:0 w:128:128:256:0 ;;
+    kprof)   # kernel trace of the kbench specs in KPROF_SPECS
+      ROOT=$(pwd); export TMPDIR=/tmp; rm -rf gpurun_out/kprof
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$ROOT/gpurun_out/kprof" -o run -- python "$ROOT/tools/kbench.py" --iters 5 ${KPROF_SPECS} ) \
+          > gpurun_out/kprof.log 2>&1
+      rc=$?; echo "kprof rc=$rc"; tail -n 3 gpurun_out/kprof.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    pdsweep) run pdsweep 900 bash tools/pd_sweep.sh ;;
     opprof) run opprof 300 python tools/op_profile.py --json gpurun_out/opprof.json ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     *) echo "unknown step $step"; exit 2 ;;
