@@ -706,7 +706,7 @@ struct WgBParams {
   int ups;
   float scale;
   int NB, TH, TW, tiles_x, tiles_y, ntiles, tiles_per_split;
-  int GZS, HS, halo_elems;
+  int GZS, HS, halo_elems, hpad;
   // PG_CONV_GZ_BITS: gz at half resolution, masked by lrelu'(gzb) at full resolution
   const unsigned char* gzb;
   int gzb_cs;
@@ -732,9 +732,13 @@ void wgrad_bf16_kernel(WgBParams p) {
   bf16_t* gzl = reinterpret_cast<bf16_t*>(smem);
   // row r of a tile lives at r*S + (r/8)*64 elements: with S = 16 (mod 32) elements the
   // transposed fragment reads are bank-conflict free (tools/lds_banks.py)
-  constexpr int GZS = BO + (BO > 16 ? 16 : 0), HS = BC + (BC > 16 ? 16 : 0);
+  // halo rows: BC = 16 unpadded, plus p.hpad elements per 8 rows (64 for 16- and 8-wide
+  // tiles, 0 for 4x4): 1 LDS cycle per 32-lane group on the tap-shifted reads at 16x8
+  // tiles, was 2 with 48-byte rows (tools/lds_banks.py wgrad_halo)
+  constexpr int GZS = BO + (BO > 16 ? 16 : 0), HS = BC == 16 ? 16 : BC + 16;
+  const int hpad = p.hpad;
   auto grow = [](int r) { return r * GZS + (r >> 3) * 64; };
-  auto hrow = [](int r) { return r * HS + (r >> 3) * 64; };
+  auto hrow = [hpad](int r) { return r * HS + (r >> 3) * hpad; };
   bf16_t* hal = gzl + grow(WGB_BP);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid % KW, wmn = wid / KW;
@@ -1087,7 +1091,8 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.ntiles = pl.ntiles;
   p.tiles_per_split = pl.tiles_per_split;
   p.GZS = BO + (BO > 16 ? 16 : 0);
-  p.HS = BC + (BC > 16 ? 16 : 0);
+  p.HS = BC == 16 ? 16 : BC + 16;
+  p.hpad = pl.tc.TW >= 8 ? 64 : 0;
   p.halo_elems = pl.tc.NB * (pl.tc.TH + 2) * (pl.tc.TW + 2);
   p.gzb = (d->flags & PG_CONV_GZ_BITS) ? reinterpret_cast<const unsigned char*>(gzbits) : nullptr;
   p.gzb_cs = d->xb_cs;
@@ -1105,7 +1110,7 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   } else {
     p.mode = WG_ATOMIC;
   }
-  int lds = (WGB_BP * p.GZS + (WGB_BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * 64) * 2;
+  int lds = (WGB_BP * p.GZS + (WGB_BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2;
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);

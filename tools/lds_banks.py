@@ -68,3 +68,33 @@ if __name__ == "__main__":
     for BO in (16, 32, 64):
         for pad in (0, 4, 8, 16, 24):
             print(f"  GZS {BO + pad}:", wgrad(BO + pad, BO + pad, 16, 8))
+
+
+def wgrad_halo(HS, PADE, TW, TH, BP=128):
+    """Tap-shifted halo reads of wgrad_bf16_kernel: halo row h at h*HS + (h//8)*PADE elements;
+    mean LDS cycles per 32-lane group (1.0 = conflict free)."""
+    TW2 = TW + 2
+    tot = n = 0
+    for ks in range(BP // 32):
+        for half in (0, 4):
+            for tap in range(9):
+                toff = (tap // 3) * TW2 + tap % 3
+                addrs = []
+                for lane in range(64):
+                    g, i16 = lane >> 4, lane & 15
+                    q, pq = i16 >> 2, i16 & 3
+                    rA = ks * 32 + 8 * g + q + half
+                    tx, ty, nb = rA % TW, (rA // TW) % TH, rA // (TW * TH)
+                    h = (nb * (TH + 2) + ty) * TW2 + tx + toff
+                    addrs.append((h * HS + (h // 8) * PADE + 4 * pq) * 2)
+                c, grp = cycles(addrs, 8)
+                tot += c
+                n += grp
+    return tot / n
+
+
+if __name__ == "__main__":
+    print("wgrad halo (rows of BC=16 / 32 channels):")
+    for TW, TH in ((16, 8), (8, 8), (4, 4)):
+        for HS in (16, 32, 48):
+            print(f"  TW {TW} HS {HS}:", {P: round(wgrad_halo(HS, P, TW, TH), 3) for P in (0, 32, 64)})
