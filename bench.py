@@ -29,6 +29,9 @@ PAPER_DEPTHS = [512, 512, 512, 512, 256, 128, 64, 32, 16]
 # dense peaks, /opt/skills/guides/MI355X_MICROARCH.md (chip-level parameters)
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}
 PEAK_HBM_GBS = 8000.0
+# minimal algorithmic GFLOP per image of the step (counted over the reference's
+# own train_step incl. the double backward, without the discarded D wgrad of the G half)
+STEP_GFLOP_PER_IMG = {5: 626.63, 6: 844.33, 7: 1062.29, 8: 1280.78}
 
 
 def parse():
@@ -48,18 +51,25 @@ def parse():
 
 def conv_bytes(x, wpk, y, kw):
     """Algorithmic HBM bytes of one conv3x3 launch: input (at its stored resolution), output
-    (read too when accumulating), the mask operand, the second output, packed weights."""
+    (read too when accumulating), the mask operand, the second output, the input sign bits,
+    packed weights -- each at its own element size (bf16 activations, uint8 sign bits)."""
     B, H, W, fl = kw["B"], kw["H"], kw["W"], kw["flags"]
-    es = y.element_size()
     hin = H // 2 if fl & 1 else H
     ho = H // 2 if fl & 16 else H
-    n = B * hin * (W // 2 if fl & 1 else W) * x.shape[-1]
-    n += B * ho * (W // 2 if fl & 16 else W) * y.shape[-1] * (2 if fl & 32 else 1)
-    if kw.get("aux") is not None:
-        n += B * H * W * kw["aux"].shape[-1]
-    if kw.get("y2") is not None:
-        n += B * ho * (W // 2 if fl & 16 else W) * kw["y2"].shape[-1]
-    return n * es + wpk.numel() * wpk.element_size()
+    wo = W // 2 if fl & 16 else W
+    n = B * hin * (W // 2 if fl & 1 else W) * x.shape[-1] * x.element_size()
+    n += B * ho * wo * y.shape[-1] * y.element_size() * (2 if fl & 32 else 1)
+    aux = kw.get("aux")
+    if aux is not None:
+        n += B * H * W * aux.shape[-1] * aux.element_size()
+    y2 = kw.get("y2")
+    if y2 is not None:
+        n += B * H * W * y2.shape[-1] * y2.element_size() if y2.dim() == 4 and y2.shape[1] == H \
+            else y2.numel() * y2.element_size()
+    xb = kw.get("xbits")
+    if xb is not None:
+        n += B * H * W * xb.shape[-1] * xb.element_size()
+    return n + wpk.numel() * wpk.element_size()
 
 
 class KernelTimer:
@@ -316,6 +326,11 @@ def main():
                         launches_per_step=kd["launches"],
                         avg_launch_us=round(kd["avg_us"], 2),
                         roofline_time_frac=round(kd["roofline_time_frac"], 4),
+                        # whole-step MFMA fraction at the minimal algorithmic
+                        # 1280.78 GFLOP per image (C5), all kernels, wall clock
+                        step_mfma_frac=round(STEP_GFLOP_PER_IMG.get(args.stage, 0.0) * 1e9 *
+                                             B * args.steps / dt /
+                                             (PEAK_TFLOPS[args.dtype] * 1e12), 4),
                         kernels={k: dict(total_ms_per_step=round(v["total_ms"], 3),
                                          tflops=round(v["tflops"], 2), gbps=round(v["gbps"], 1),
                                          roofline_time_frac=round(v["roofline_time_frac"], 4),
