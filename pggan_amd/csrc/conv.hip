@@ -707,6 +707,7 @@ struct WgBParams {
   float scale;
   int NB, TH, TW, tiles_x, tiles_y, ntiles, tiles_per_split;
   int GZS, HS, halo_elems, hpad;
+  int lg_tx, lg_ty;   // log2 of tiles_x / tiles_y, -1 when not a power of two
   // PG_CONV_GZ_BITS: gz at half resolution, masked by lrelu'(gzb) at full resolution
   const unsigned char* gzb;
   int gzb_cs;
@@ -766,7 +767,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   // halo element k -> packed (image, hy, hx, channel vector) or -1
   constexpr bool gz_bits = GZB;   // gz = up2(g) * lrelu'(bits) (PG_CONV_GZ_BITS)
   const int gH = gz_bits ? p.H >> 1 : p.H, gW = gz_bits ? p.W >> 1 : p.W;
-  int gzrel[NGZ], gznb[NGZ], hpk[NH], gbrel[NGZ];
+  int gzrel[NGZ], gznb[NGZ], hpk[NH], gbrel[NGZ], hrel[NH];
 #pragma unroll
   for (int k = 0; k < NGZ; ++k) {
     const int i = tid + k * 256;
@@ -787,15 +788,23 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int hy = rem / TW2, hx = rem - hy * TW2;
       if (c0 + 8 * v < p.x_cs) hpk[k] = (nb << 24) | (hy << 16) | (hx << 8) | v;
     }
+    // element offset from the tile's input origin (tile origins are even, so the
+    // upsample's floor shift splits: (t0 + h - 1) >> 1 = t0 / 2 + ((h - 1) >> 1))
+    const int pk = hpk[k] < 0 ? 0 : hpk[k];
+    const int ys = p.ups ? 1 : 0;
+    if constexpr (MO < 4) hrel[k] = (((pk >> 24) * p.Hin + ((((pk >> 16) & 0xff) - 1) >> ys)) * p.Win +
+               ((((pk >> 8) & 0xff) - 1) >> ys)) * p.x_cs + 8 * (pk & 0xff);
   }
   // ok masks of a loaded tile: bit k of gz vector k / halo vector k (zero fill at the
   // LDS write, so the loaded registers are not touched before then)
   auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH], int (&rb)[NGZ],
                        unsigned& gok, unsigned& hok) {
-    const int tx0 = (t % p.tiles_x) * p.TW;
-    int tt = t / p.tiles_x;
-    const int ty0 = (tt % p.tiles_y) * p.TH;
-    const int b0 = (tt / p.tiles_y) * p.NB;
+    // tile -> origin (wave-uniform, scalar; shifts where the tile counts are powers of 2)
+    constexpr bool sh = MO < 4;   // A/B: shifts help the narrow tiles, not the wide ones
+    const int tx0 = (sh && p.lg_tx >= 0 ? (t & (p.tiles_x - 1)) : t % p.tiles_x) * p.TW;
+    const int tt = sh && p.lg_tx >= 0 ? t >> p.lg_tx : t / p.tiles_x;
+    const int ty0 = (sh && p.lg_ty >= 0 ? (tt & (p.tiles_y - 1)) : tt % p.tiles_y) * p.TH;
+    const int b0 = (sh && p.lg_ty >= 0 ? tt >> p.lg_ty : tt / p.tiles_y) * p.NB;
     const int gs = gz_bits ? 1 : 0;
     gok = 0;
     hok = 0;
@@ -811,17 +820,23 @@ void wgrad_bf16_kernel(WgBParams p) {
       gok |= (ok ? 1u : 0u) << k;
     }
     const int ys = p.ups ? 1 : 0;
-    const bf16_t* xb = p.x + c0;
+    // the tile's input origin (scalar) + the lane's precomputed offset
+    const bf16_t* xt = MO < 4 ? p.x + c0 + (((size_t)b0 * p.Hin + (ty0 >> ys)) * p.Win + (tx0 >> ys)) * p.x_cs
+                              : p.x;
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
       const int pk = hpk[k];
-      const int b = b0 + (pk >> 24), yy = ty0 + ((pk >> 16) & 0xff) - 1,
-                xx = tx0 + ((pk >> 8) & 0xff) - 1;
-      const bool ok =
-          pk >= 0 && b < p.B && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      rh[k] = *reinterpret_cast<const u32x4_t*>(
-          ok ? xb + (((size_t)b * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs + 8 * (pk & 0xff)
-             : p.x);
+      const int yy = ty0 + ((pk >> 16) & 0xff) - 1, xx = tx0 + ((pk >> 8) & 0xff) - 1;
+      const bool ok = pk >= 0 && b0 + (pk >> 24) < p.B && (unsigned)yy < (unsigned)p.H &&
+                      (unsigned)xx < (unsigned)p.W;
+      if constexpr (MO < 4) {   // precomputed offsets (A/B: -7..-13 % at 1024^2)
+        rh[k] = *reinterpret_cast<const u32x4_t*>(ok ? xt + hrel[k] : p.x);
+      } else {                  // wide tiles: registers are tighter than VALU (+2 % the other way)
+        rh[k] = *reinterpret_cast<const u32x4_t*>(
+            ok ? p.x + c0 + (((size_t)(b0 + (pk >> 24)) * p.Hin + (yy >> ys)) * p.Win + (xx >> ys)) * p.x_cs +
+                     8 * (pk & 0xff)
+               : p.x);
+      }
       hok |= (ok ? 1u : 0u) << k;
     }
   };
@@ -1088,6 +1103,9 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.NB = pl.tc.NB; p.TH = pl.tc.TH; p.TW = pl.tc.TW;
   p.tiles_x = d->W / pl.tc.TW;
   p.tiles_y = d->H / pl.tc.TH;
+  auto lg2 = [](int v) { int l = 0; while ((1 << l) < v) ++l; return (1 << l) == v ? l : -1; };
+  p.lg_tx = lg2(p.tiles_x);
+  p.lg_ty = lg2(p.tiles_y);
   p.ntiles = pl.ntiles;
   p.tiles_per_split = pl.tiles_per_split;
   p.GZS = BO + (BO > 16 ? 16 : 0);

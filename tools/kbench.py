@@ -73,10 +73,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="library to load instead of the in-tree build")
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the spec list (A/B interleaving)")
     ap.add_argument("specs", nargs="+")
     a = ap.parse_args()
+    if a.lib:
+        _lib.load_library(a.lib)
     ops = _lib.HipOps(torch.bfloat16)
-    for s in a.specs:
+    for s in a.specs * a.rounds:
         try:
             run(ops, s, a.B, a.iters)
         except RuntimeError as e:   # e.g. a tuning override with no kernel for the plan
