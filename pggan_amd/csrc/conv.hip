@@ -901,17 +901,29 @@ void wgrad_bf16_kernel(WgBParams p) {
         A[mo] = tr_read8(gzl + grow(rA) + ol, gzl + grow(rB) + ol);
       }
       const int hA = hAo[j], hB = hBo[j];
+      auto readB = [&](int tap, int nc) {
+        const int toff = (tap / 3) * TW2 + (tap % 3);
+        const int cl = (wc * NC + nc) * 16 + 4 * pq;
+        return tr_read8(hal + hrow(hA + toff) + cl, hal + hrow(hB + toff) + cl);
+      };
+      // software-pipelined: the B fragment of the next (tap, nc) is read before the MFMAs
+      // of the current one, so they never wait on a read issued just before them
+      bf16x8_t Bc = readB(0, 0);
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int toff = (tap / 3) * TW2 + (tap % 3);
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
-          const int cl = (wc * NC + nc) * 16 + 4 * pq;
-          const bf16x8_t Bf = tr_read8(hal + hrow(hA + toff) + cl, hal + hrow(hB + toff) + cl);
+          const bool last = tap == 8 && nc == NC - 1;
+          const bf16x8_t Bn = last ? Bc : (nc + 1 < NC ? readB(tap, nc + 1) : readB(tap + 1, 0));
+          // keep the read ahead of these MFMAs (wide tiles; A/B: -2..-12 % there, +15 % at
+          // MO = 1 where one MFMA per read cannot cover it)
+          if constexpr (MO >= 4) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int mo = 0; mo < MO; ++mo)
-            acc[mo][nc][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mo], Bf, acc[mo][nc][tap],
+            acc[mo][nc][tap] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[mo], Bc, acc[mo][nc][tap],
                                                                        0, 0, 0);
+          if constexpr (MO >= 4) __builtin_amdgcn_sched_barrier(0);
+          Bc = Bn;
         }
       }
     }
