@@ -1315,8 +1315,14 @@ int conv_splits(const pg_conv_desc* d) {
   const int base = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH) * pg_cdiv(cout_p, BN);
   const int cin_p = cinp_of(d->cin);
   const int nch = cin_p / (cin_p < 32 ? cin_p : 32);
-  if (base >= 128 || nch < 4) return 1;
-  int sp = pg_cdiv(256, base);
+  // PG_CONV_SPLIT="min_base,target" overrides for tuning runs
+  static int min_base = -1, target = 256;
+  if (min_base < 0) {
+    min_base = 128;
+    if (const char* e = getenv("PG_CONV_SPLIT")) sscanf(e, "%d,%d", &min_base, &target);
+  }
+  if (base >= min_base || nch < 4) return 1;
+  int sp = pg_cdiv(target, base);
   if (sp > nch) sp = nch;
   const int cps = pg_cdiv(nch, sp);
   return pg_cdiv(nch, cps);
