@@ -26,6 +26,7 @@ images NCHW fp32, parameters/gradients/Adam state fp32 in flat buffers.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -172,7 +173,8 @@ class StepEngine:
         self.keep_fake_D = False
         self.fuse_pixnorm = True   # PixelNorm in the G conv epilogues where the kernel allows
         self.fuse_dbits = True     # D conv+lrelu+pool outputs kept as sign bits (see _dbits)
-        self.dbits_min_res = 512
+        # tuning runs only: PG_DBITS_MIN_RES (sign-bit D activations from this resolution)
+        self.dbits_min_res = int(os.environ.get("PG_DBITS_MIN_RES", "512"))
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
         self._alloc()
