@@ -714,21 +714,23 @@ struct WgBParams {
   float slope;
 };
 
-constexpr int WGB_BP = 128;        // pixels per staged tile
-constexpr int WGB_MAXHALO = 288;   // max halo pixels of a 128-pixel tile (pick_tile, W = 4)
+// pixels per staged tile: 128, or 256 (16x16) for the wide tiles at W >= 16 (half the
+// per-tile staging / barrier overhead per MFMA)
+constexpr int WGB_BP = 128;
+constexpr int wgb_maxhalo(int bp) { return bp == 128 ? 288 : 18 * 18; }   // pick_tile geometry
 
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
-template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB>
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB, int BP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void wgrad_bf16_kernel(WgBParams p) {
   constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
   constexpr int GV = BO / 8, HV = BC / 8;
-  constexpr int NGZ = WGB_BP * GV / 256;                  // gz vectors per thread
-  constexpr int NH = (WGB_MAXHALO * HV + 255) / 256;      // halo vectors per thread (max)
-  static_assert(NGZ * 256 == WGB_BP * GV, "gz staging must tile the workgroup");
+  constexpr int NGZ = BP * GV / 256;                      // gz vectors per thread
+  constexpr int NH = (wgb_maxhalo(BP) * HV + 255) / 256;  // halo vectors per thread (max)
+  static_assert(NGZ * 256 == BP * GV, "gz staging must tile the workgroup");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* gzl = reinterpret_cast<bf16_t*>(smem);
   // row r of a tile lives at r*S + (r/8)*64 elements: with S = 16 (mod 32) elements the
@@ -740,7 +742,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   const int hpad = p.hpad;
   auto grow = [](int r) { return r * GZS + (r >> 3) * 64; };
   auto hrow = [hpad](int r) { return r * HS + (r >> 3) * hpad; };
-  bf16_t* hal = gzl + grow(WGB_BP);
+  bf16_t* hal = gzl + grow(BP);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid % KW, wmn = wid / KW;
   const int wo = wmn / WNC, wc = wmn % WNC;
@@ -878,7 +880,7 @@ void wgrad_bf16_kernel(WgBParams p) {
     }
   };
   // halo rows of this lane's two k-rows for each k-step the wave owns (tile-invariant)
-  constexpr int KSW = (WGB_BP / 32) / KW;
+  constexpr int KSW = (BP / 32) / KW;
   int hAo[KSW], hBo[KSW];
 #pragma unroll
   for (int j = 0; j < KSW; ++j) {
@@ -1059,7 +1061,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t
 }
 
 struct WgbPlan {
-  int MO, NC, WMO, WNC;
+  int MO, NC, WMO, WNC, BP;
   int ot, ct, splits, tiles_per_split, ntiles;
   TileCfg tc;
   size_t slab;
@@ -1073,7 +1075,13 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   pl.WMO = 1;
   pl.WNC = ci <= 16 ? 1 : ci <= 32 ? 2 : 1;
   const int BO = pl.WMO * pl.MO * 16, BC = pl.WNC * pl.NC * 16;
-  pl.tc = pick_tile(d->H, d->W, WGB_BP, 32);
+  // A/B (tools/wgbp_ab.sh): 256-pixel tiles -6..-10 % at 32^2-128^2 (cin > 32), neutral at
+  // 256^2, +50 % at 512^2 32->64 (the WNC = 2 tile spills)
+  const bool bp256_ok = pl.MO >= 4 && pl.WNC == 1 && d->W >= 16 && d->H >= 16 && d->W <= 128 &&
+                        !(d->flags & PG_CONV_GZ_BITS);
+  pl.BP = bp256_ok ? 256 : WGB_BP;
+  if (const char* e = getenv("PG_WG_BP")) pl.BP = (atoi(e) == 256 && bp256_ok) ? 256 : 128;   // tuning
+  pl.tc = pick_tile(d->H, d->W, pl.BP, 32);
   pl.ntiles = pg_cdiv(d->B, pl.tc.NB) * (d->W / pl.tc.TW) * (d->H / pl.tc.TH);
   pl.ot = pg_cdiv(co, BO);
   pl.ct = pg_cdiv(ci, BC);
@@ -1099,7 +1107,7 @@ size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
   return pl.splits > 1 ? pl.splits * pl.slab * sizeof(float) : 0;
 }
 
-template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false>
+template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false, int BP = WGB_BP>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
                       float scale, float* dw, float* db, float* ws, size_t ws_bytes,
                       hipStream_t st, const void* gzbits) {
@@ -1129,7 +1137,8 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.slope = d->slope;
   PG_CHECK_ARG(!p.gzb || (d->xb_cs * 8 >= d->cout && pl.tc.TH % 2 == 0 && pl.tc.TW % 2 == 0),
                "wgrad_bf16: GZ_BITS needs gzbits with >= cout/8 bytes per pixel");
-  PG_CHECK_ARG(p.halo_elems <= WGB_MAXHALO, "wgrad_bf16: halo %d > %d", p.halo_elems, WGB_MAXHALO);
+  PG_CHECK_ARG(pl.BP == BP && p.halo_elems <= wgb_maxhalo(BP), "wgrad_bf16: halo %d > %d", p.halo_elems,
+               wgb_maxhalo(BP));
   p.slab = pl.slab;
   p.ws = nullptr;
   if (pl.splits == 1) {
@@ -1140,17 +1149,17 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   } else {
     p.mode = WG_ATOMIC;
   }
-  int lds = (WGB_BP * p.GZS + (WGB_BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2;
+  int lds = (BP * p.GZS + (BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2;
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB>,
+    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_done = true;
   }
-  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB>), dim3(pl.ot, pl.ct, pl.splits),
+  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   if (p.mode == WG_SLABS) {
@@ -1190,6 +1199,12 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
       if (gzb)                                                                             \
         return launch_wgrad_bf16<a, b, c, e, PD, WPE, true>(d, pl, x, gz, scale, dw, db,   \
                                                             ws, ws_bytes, st, gzbits);     \
+    }                                                                                      \
+    if constexpr (a == 4) {                                                                \
+      if (pl.BP == 256 && !gzb)                                                            \
+        return launch_wgrad_bf16<a, b, c, e, PD, WPE, false, 256>(d, pl, x, gz, scale, dw, \
+                                                                  db, ws, ws_bytes, st,    \
+                                                                  gzbits);                 \
     }                                                                                      \
     PG_CHECK_ARG(!gzb, "wgrad_bf16: GZ_BITS not instantiated for this tile");              \
     return launch_wgrad_bf16<a, b, c, e, PD, WPE, false>(d, pl, x, gz, scale, dw, db, ws,  \
