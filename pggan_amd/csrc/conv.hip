@@ -492,8 +492,62 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
 
 // Split-K reduction + epilogue: y = out_scale * post(sum_z slab_z + bias) with the same
 // flag semantics as conv3x3_kernel's epilogue (bias, lrelu, 2x2 pool (+ y2), mask, accum).
+// PIXNORM (no pool / mask / accumulate): one wave per pixel, the wave's lanes hold all
+// cout channels (4 per lane and round); bias, leaky relu, bf16 rounding as stored, then
+// y = v * r with r = rsqrt(mean_c v^2 + 1e-8) (lib/layers.py:8-14), r to y2 (fp32 per pixel)
+template <typename T>
+__device__ void splitk_pixnorm(const ConvParams& p, int splits) {
+  const int lane = threadIdx.x & 63;
+  const int npix = p.B * p.H * p.W;
+  const int pix = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (pix >= npix) return;   // wave-uniform
+  constexpr int MAXR = 4;    // cout <= 1024
+  float v[MAXR][4];
+  float ss = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < MAXR; ++rr) {
+    const int c = (rr * 64 + lane) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[rr][q] = 0.f;
+    if (c >= p.cout) continue;
+    const float* src = p.ws + (size_t)pix * p.cout_p + c;
+    float a[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] = (p.flags & PG_CONV_BIAS) ? p.bias[c + q] : 0.f;
+    for (int z = 0; z < splits; ++z) {
+      const f32x4_t t = *reinterpret_cast<const f32x4_t*>(src + z * p.slab);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] += t[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float u = (p.flags & PG_CONV_LRELU) ? lrelu_f(a[q], p.slope) : a[q];
+      if constexpr (sizeof(T) == 2) u = bf2f(f2bf(u));
+      v[rr][q] = u;
+      ss += u * u;
+    }
+  }
+  ss = wave_sum(ss);
+  const float rn = rsqrtf(ss / (float)p.cout + 1e-8f);
+  T* y = reinterpret_cast<T*>(p.y);
+#pragma unroll
+  for (int rr = 0; rr < MAXR; ++rr) {
+    const int c = (rr * 64 + lane) * 4;
+    if (c >= p.cout) continue;
+    float o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = v[rr][q] * rn;
+    Ty<T>::st4(y + (size_t)pix * p.y_cs + c, o);
+  }
+  if (p.y2 && lane == 0) reinterpret_cast<float*>(p.y2)[pix] = rn;
+}
+
 template <typename T>
 __global__ void conv_splitk_epilogue(ConvParams p, int splits) {
+  if (p.flags & PG_CONV_PIXNORM) {
+    splitk_pixnorm<T>(p, splits);
+    return;
+  }
   const int nv = p.cout >> 2;
   const bool pool = (p.flags & PG_CONV_POOL) != 0;
   const int Ho = pool ? p.H >> 1 : p.H, Wo = pool ? p.W >> 1 : p.W;
@@ -1412,6 +1466,10 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
     const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
     int blocks = (int)((n + 255) / 256);
     if (blocks > 8192) blocks = 8192;
+    if (d->flags & PG_CONV_PIXNORM) {   // one wave per pixel
+      PG_CHECK_ARG(d->cout <= 1024 && d->cout % 4 == 0, "conv3x3: split-K PixelNorm needs cout %% 4 == 0, <= 1024");
+      blocks = pg_cdiv(d->B * d->H * d->W, 4);
+    }
     hipLaunchKernelGGL(conv_splitk_epilogue<T>, dim3(blocks), dim3(256), 0, st, p, splits);
   }
   PG_LAUNCH_CHECK();
@@ -1464,7 +1522,9 @@ bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   conv_tile_for(d->cout, &BM, &BN, d->W);
   const size_t need = conv_ws_bytes(d);
   const bool split = need && wsb >= need && conv_splits(d) > 1;
-  return BN <= 32 && cout_p <= BN && !split;   // [cout][pixel] variants, single pass
+  // in the split-K epilogue (bf16 step; the fp32 parity mode keeps PixelNorm separate)
+  if (split) return sizeof(T) == 2 && BN == 64 && d->cout % 4 == 0 && d->cout <= 1024;
+  return BN <= 32 && cout_p <= BN;   // [cout][pixel] variants, single pass
 }
 
 template <typename T>

@@ -194,6 +194,7 @@ class StepEngine:
         g["h0"] = t(B, 4, 4, d[0])
         g["u0"] = t(B, 4, 4, d[0])
         g["y0"] = t(B, 4, 4, d[0])
+        g["r0"] = t(B, 4, 4, 1, f32=True)
         for i in range(s):
             Ri = 8 * 2 ** i
             for k in ("ua", "ya", "ub", "yb", "gzb", "gya", "gza"):
@@ -423,8 +424,8 @@ class StepEngine:
                    flags=L.LIN_BIAS | L.LIN_LRELU | L.LIN_OUT_CHW, scale=he(self.latent),
                    slope=self.hyper.slope_cfg)                                # :129-130
         ops.pixnorm(g["f"], g["h0"], d[0])                                   # :132-133
-        self._conv("G", "first", g["h0"], g["u0"], 4, d[0], d[0], L.CONV_LRELU)
-        ops.pixnorm(g["u0"], g["y0"], d[0])                                  # blocks.py:131-139
+        self._g_conv_pn("first", g["h0"], g["u0"], g["y0"], g["r0"], 4, d[0], d[0], L.CONV_LRELU,
+                        keep)                                                # blocks.py:131-139
         prev = g["y0"]
         for i in range(s):                                                   # nets.py:144-149
             Ri = 8 * 2 ** i
@@ -480,7 +481,8 @@ class StepEngine:
             self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
                        dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
         fb = "first_block.block.0.module."
-        ops.pixnorm_lrelu_bwd(g["u0"], g["gy0"], g["gz0"], d[0], SLOPE)
+        self._g_pn_bwd("first", g["u0"], g["y0"], g["r0"], g["gy0"], g["gz0"], 4, d[0], d[0],
+                       L.CONV_LRELU)
         self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
                     db=GR[fb + "bias"])
         self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)

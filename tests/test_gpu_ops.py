@@ -360,15 +360,19 @@ def test_randn_moments():
                                   (4, 4, 513, 512, ("bias", "lrelu")),
                                   (4, 4, 512, 516, ()),
                                   (4, 8, 512, 512, ("mask", "accum")),
-                                  (3, 8, 256, 64, ("ups", "bias", "lrelu"))])
+                                  (3, 8, 256, 64, ("ups", "bias", "lrelu")),
+                                  (4, 8, 512, 512, ("ups", "bias", "lrelu", "pixnorm")),
+                                  (4, 4, 512, 512, ("bias", "lrelu", "pixnorm"))])
 def test_conv3x3_splitk(case, dtype):
-    """Small-spatial wide convs take the split-K path (fp32 partial slabs + epilogue)."""
+    """Small-spatial wide convs take the split-K path (fp32 partial slabs + epilogue; the
+    generator's PixelNorm runs in that epilogue, y2 = the per-pixel factor)."""
     B, H, cin, cout, fl = case
     _L = lib()
     hip, cpu = ops_pair(dtype)
     flags = 0
     for f, v in (("ups", _L.CONV_UPS_IN), ("bias", _L.CONV_BIAS), ("lrelu", _L.CONV_LRELU),
-                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM)):
+                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM),
+                 ("pixnorm", _L.CONV_PIXNORM)):
         if f in fl:
             flags |= v
     need = hip.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
@@ -388,6 +392,12 @@ def test_conv3x3_splitk(case, dtype):
         ops.conv_pack(0, w.to(dev), 0.02, wp)
         y = y0.to(dev).to(dt).clone()
         y2 = torch.zeros(B, H, H, cout, dtype=dt, device=dev) if "pool" in fl else None
+        if "pixnorm" in fl:
+            if dtype != torch.bfloat16:
+                pytest.skip("split-K PixelNorm is a bf16-step fusion")
+            y2 = torch.zeros(B, H, H, dtype=torch.float32, device=dev)
+            assert ops.conv_supported(B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
+                                      ws_bytes=need), "split-K PixelNorm expected"
         ws = torch.empty(need // 4, device=dev) if dev == "cuda" else None
         ops.conv3x3(x.to(dev).to(dt), wp, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
                     out_scale=0.25 if "pool" in fl else 1.0, bias=(bias * 0.02).to(dev),
