@@ -1127,11 +1127,16 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   pl.MO = co <= 16 ? 1 : co <= 32 ? 2 : 4;
   pl.NC = 1;
   pl.WMO = 1;
-  pl.WNC = ci <= 16 ? 1 : ci <= 32 ? 2 : 1;
+  // two 16-channel halves of a 32-channel input slice per workgroup (waves split the
+  // channels, the gz tile is staged once for both): A/B -5..-22 % at 32^2-256^2 for
+  // cin > 32; below 32^2 the single-half tile is faster
+  pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32) ? 2 : 1;
+  if (const char* e = getenv("PG_WG_WNC")) { if (ci > 16) pl.WNC = atoi(e); }   // tuning runs only
   const int BO = pl.WMO * pl.MO * 16, BC = pl.WNC * pl.NC * 16;
-  // A/B (tools/wgbp_ab.sh): 256-pixel tiles -6..-10 % at 32^2-128^2 (cin > 32), neutral at
-  // 256^2, +50 % at 512^2 32->64 (the WNC = 2 tile spills)
-  const bool bp256_ok = pl.MO >= 4 && pl.WNC == 1 && d->W >= 16 && d->H >= 16 && d->W <= 128 &&
+  // A/B (tools/wgbp_ab.sh): 256-pixel tiles -6..-10 % at 32^2-128^2 for the single-half
+  // (WNC = 1) tile, but the two-half tile is faster still there (tools/wnc_sweep.sh), so
+  // the default never picks them; PG_WG_BP=256 for tuning; +50 % with WNC = 2 (spills)
+  const bool bp256_ok = pl.MO >= 4 && pl.WNC == 1 && d->W >= 32 && d->H >= 32 && d->W <= 128 &&
                         !(d->flags & PG_CONV_GZ_BITS);
   pl.BP = bp256_ok ? 256 : WGB_BP;
   if (const char* e = getenv("PG_WG_BP")) pl.BP = (atoi(e) == 256 && bp256_ok) ? 256 : 128;   // tuning
