@@ -1331,15 +1331,23 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const pg_pack_item* ite
   __syncthreads();
   T* fwd = reinterpret_cast<T*>(it.fwd);
   T* dg = reinterpret_cast<T*>(it.dgrad);
-  for (int i = tid; i < 32 * 288; i += 256) {
-    const int cl = i & 31, tap = (i >> 5) % 9, ol = i / 288;
-    const int o = o0 + ol, c = c0 + cl;
-    if (o < rf && c < kf) Ty<T>::st(fwd + ((size_t)o * 9 + tap) * kf + c, s[ol][cl * 9 + tap]);
+  // 4 consecutive fastest-axis elements per store (kf, kd, rf, rd are multiples of 16, so a
+  // group of 4 is wholly inside or outside the padded range and 8/16-byte aligned)
+  for (int i = tid; i < 8 * 288; i += 256) {
+    const int cq = i & 7, tap = (i >> 3) % 9, ol = i / 72;
+    const int o = o0 + ol, c = c0 + 4 * cq;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = s[ol][(4 * cq + k) * 9 + tap];
+    if (o < rf && c < kf) Ty<T>::st4(fwd + ((size_t)o * 9 + tap) * kf + c, v);
   }
-  for (int i = tid; i < 32 * 288; i += 256) {
-    const int ol = i & 31, tap = (i >> 5) % 9, cl = i / 288;
-    const int o = o0 + ol, c = c0 + cl;
-    if (c < rd && o < kd) Ty<T>::st(dg + ((size_t)c * 9 + tap) * kd + o, s[ol][cl * 9 + 8 - tap]);
+  for (int i = tid; i < 8 * 288; i += 256) {
+    const int oq = i & 7, tap = (i >> 3) % 9, cl = i / 72;
+    const int o = o0 + 4 * oq, c = c0 + cl;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = s[4 * oq + k][cl * 9 + 8 - tap];
+    if (c < rd && o < kd) Ty<T>::st4(dg + ((size_t)c * 9 + tap) * kd + o, v);
   }
   if (c0 == 0 && tid < 32 && o0 + tid < cout)
     it.bias_scaled[o0 + tid] = it.bias ? it.bias[o0 + tid] * it.scale : 0.f;
