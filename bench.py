@@ -37,8 +37,8 @@ STEP_GFLOP_PER_IMG = {5: 626.63, 6: 844.33, 7: 1062.29, 8: 1280.78}
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--stage", type=int, default=8)
     p.add_argument("--batch", type=int, default=4)
     p.add_argument("--alpha", type=float, default=1.0)

@@ -68,6 +68,13 @@ int pg_version(void);
                                  (pg_conv3x3_fwd_ex; xb_cs = bytes per pixel) */
 #define PG_CONV_GZ_BITS 1024  /* wgrad: gz is at H/2 x W/2 and the effective gradient is
                                  up2(gz) * lrelu'(gzbits) (pg_conv3x3_wgrad_ex) */
+/* PixelNorm + LReLU backward fused into an input-gradient conv (bf16, H,W >= 16 kernel; query
+ * pg_conv3x3_supported): with v the conv result = dL/dy of a PG_CONV_PIXNORM output y, the
+ * launch writes dL/du = r * (v - y * mean_c(y * v)) * lrelu'(y), u the pre-norm activation
+ * (pg_pixnorm_lrelu_bwd_y without the round trip of v through HBM).  aux = y (storage
+ * dtype, aux_cs), y2 = r (fp32 [B*H*W], from the forward).  Not with BIAS / POOL / MASK /
+ * ACCUM / PIXNORM / bit flags. */
+#define PG_CONV_PNBWD 2048
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */

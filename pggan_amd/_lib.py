@@ -17,6 +17,7 @@ PG_F32, PG_BF16 = 0, 1
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
 CONV_PIXNORM = 64
+CONV_PNBWD = 2048
 CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (

@@ -1518,6 +1518,13 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
+  if (d->flags & PG_CONV_PNBWD) {   // conv_hr epilogue, [cout][pixel] tiles of <= 32 channels
+    if constexpr (sizeof(T) != 2) return false;
+    if (d->flags & (BITS | PG_CONV_BIAS | PG_CONV_POOL | PG_CONV_MASK | PG_CONV_ACCUM | PG_CONV_PIXNORM))
+      return false;
+    return conv_hr_ok(d) && ((d->cout + 15) & ~15) <= conv_hr_bn(d) && conv_hr_bn(d) <= 32 &&
+           d->cout % 4 == 0;
+  }
   if (d->flags & BITS) {
     if constexpr (sizeof(T) != 2) return false;
     if (!conv_hr_ok(d) || !conv_hr_mode_ok(d)) return false;
@@ -1645,8 +1652,10 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
                "conv3x3_fwd: MASK flag without aux");
   PG_CHECK_ARG(!(d->flags & PG_CONV_Y2_BITS) || (y2 && d->y2_cs * 8 >= d->cout && d->y2_cs % 2 == 0),
                "conv3x3_fwd: Y2_BITS needs y2 with >= cout/8 bytes per pixel");
-  PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM)),
-               "conv3x3_fwd: y2 only with POOL or PIXNORM");
+  PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM | PG_CONV_PNBWD)),
+               "conv3x3_fwd: y2 only with POOL, PIXNORM or PNBWD");
+  PG_CHECK_ARG(!(d->flags & PG_CONV_PNBWD) || (aux && y2 && d->aux_cs >= d->cout && d->aux_cs % 4 == 0),
+               "conv3x3_fwd: PNBWD needs aux = y (aux_cs >= cout) and y2 = r");
   PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");
   PG_CHECK_ARG(!(d->flags & PG_CONV_X_BITS), "conv3x3_fwd: X_BITS needs pg_conv3x3_fwd_ex");
   hipStream_t st = (hipStream_t)stream;

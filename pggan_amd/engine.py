@@ -175,6 +175,8 @@ class StepEngine:
         self.fuse_dbits = True     # D conv+lrelu+pool outputs kept as sign bits (see _dbits)
         # tuning runs only: PG_DBITS_MIN_RES (sign-bit D activations from this resolution)
         self.dbits_min_res = int(os.environ.get("PG_DBITS_MIN_RES", "512"))
+        # tuning / A-B runs only: PG_PNBWD=0 keeps the G PixelNorm backward as its own pass
+        self.fuse_pnbwd = os.environ.get("PG_PNBWD", "1") != "0"
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
         self._alloc()
@@ -397,6 +399,23 @@ class StepEngine:
                                          ws_bytes=need))
         return self._ws_cache[key]
 
+    def _pnb_fused(self, H, cin, cout):
+        """Whether conv a (cin -> cout, up2 input) of a generator block has its PixelNorm
+        backward fused into the input-gradient conv of conv b (cout -> cout) that produces
+        its upstream gradient: needs the fused forward (y and r stored) and a tile holding
+        every channel."""
+        key = ("pnb", H, cin, cout)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            ok = bool(self.fuse_pixnorm and self.fuse_pnbwd and f is not None and
+                      self._pn_fused(H, cin, cout, L.CONV_UPS_IN | L.CONV_LRELU))
+            if ok:
+                need = self._ws_need("c", H, cout, cout, False)
+                ok = bool(f(B=self.B, H=H, W=H, cin=cout, cout=cout, flags=L.CONV_PNBWD,
+                            ws_bytes=need))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _g_conv_pn(self, key, x, u, y, r, H, cin, cout, flags, keep):
         """conv + lrelu + PixelNorm of a generator block (lib/blocks.py:126-139): fused
         (y and, for the backward, the per-pixel factor r) or conv -> u then pixnorm -> y."""
@@ -470,10 +489,16 @@ class StepEngine:
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
                         d[i + 1],
                         db=GR[b + "bias"])
-            self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gya{i}"], Ri, d[i + 1], d[i + 1], 0,
-                       dgrad=True)
-            self._g_pn_bwd(f"a{i}", g[f"ua{i}"], g[f"ya{i}"], g[f"ra{i}"], g[f"gya{i}"],
-                           g[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_UPS_IN | L.CONV_LRELU)
+            if self._pnb_fused(Ri, d[i], d[i + 1]):
+                # conv b's input gradient with conv a's PixelNorm + LReLU backward in its
+                # epilogue (the gradient w.r.t. ya never goes through HBM)
+                self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gza{i}"], Ri, d[i + 1], d[i + 1],
+                           L.CONV_PNBWD, dgrad=True, aux=g[f"ya{i}"], y2=g[f"ra{i}"])
+            else:
+                self._conv("G", f"b{i}", g[f"gzb{i}"], g[f"gya{i}"], Ri, d[i + 1], d[i + 1], 0,
+                           dgrad=True)
+                self._g_pn_bwd(f"a{i}", g[f"ua{i}"], g[f"ya{i}"], g[f"ra{i}"], g[f"gya{i}"],
+                               g[f"gza{i}"], Ri, d[i], d[i + 1], L.CONV_UPS_IN | L.CONV_LRELU)
             self._wgrad("G", f"a{i}", self._ylvl(i), g[f"gza{i}"], GR[a + "weight"], Ri, d[i],
                         d[i + 1], ups=True,
                         db=GR[a + "bias"])

@@ -16,8 +16,9 @@ import torch.nn.functional as F
 
 CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 8, 16, 32
 CONV_PIXNORM = 64
+CONV_PNBWD = 2048
 CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
-FUSED_FLAGS = CONV_PIXNORM | CONV_Y2_BITS | CONV_AUX_BITS | CONV_X_BITS | CONV_GZ_BITS
+FUSED_FLAGS = CONV_PIXNORM | CONV_PNBWD | CONV_Y2_BITS | CONV_AUX_BITS | CONV_X_BITS | CONV_GZ_BITS
 
 
 def packbits(m):
@@ -134,6 +135,10 @@ class CpuOps:
                     y2[..., :cout] = z
             z = F.avg_pool2d(z.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4.0
         z = z * out_scale
+        if flags & CONV_PNBWD:      # PixelNorm + LReLU backward: aux = y, y2 = r
+            yv = aux[..., :cout].float()
+            r = y2.reshape(B, H, W, 1).float()
+            z = r * (z - yv * (yv * z).mean(-1, keepdim=True)) * lmask(yv, slope)
         if (flags & CONV_MASK) and not (flags & CONV_POOL):
             z = z * (bmask(aux, cout, slope) if flags & CONV_AUX_BITS else lmask(aux[..., :cout], slope))
         if flags & CONV_ACCUM:

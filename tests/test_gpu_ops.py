@@ -602,3 +602,33 @@ def test_sign_bit_conv_paths(B, H, c1, c2):
     assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
     for k in ("p", "tp", "gza", "dw", "db"):
         cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
+
+
+@pytest.mark.parametrize("B,H,C", [(2, 32, 16), (2, 64, 32), (2, 256, 16), (1, 512, 32)])
+def test_pixnorm_bwd_fused_dgrad(B, H, C):
+    """PG_CONV_PNBWD (bf16, include/pggan_hip.h): the input-gradient conv writes the
+    PixelNorm + LReLU backward of its result, r * (v - y * mean_c(y v)) * lrelu'(y), against
+    an fp32 restatement on the CPU double's conv, and against the unfused HIP pair
+    (conv -> gy in bf16 -> pg_pixnorm_lrelu_bwd_y)."""
+    from cpu_ops import CONV_PNBWD
+    hip, cpu = ops_pair(torch.bfloat16)
+    dt = torch.bfloat16
+    assert hip.conv_supported(B=B, H=H, W=H, cin=C, cout=C, flags=CONV_PNBWD)
+    gz = q(rnd(B, H, H, C, seed=91), dt)
+    wd = q(rnd(r16(C) * 9 * cinp(C), seed=92, scale=0.05), dt)
+    u = rnd(B, H, H, C, seed=93)
+    r = torch.rsqrt((u * u).mean(-1) + 1e-8)
+    y = q(u * r[..., None], dt)
+    v = torch.zeros(B, H, H, C)
+    cpu.conv3x3(gz, wd, v, B=B, H=H, W=H, cin=C, cout=C, flags=0)
+    ref = r[..., None] * (v - y * (y * v).mean(-1, keepdim=True)) * torch.where(y > 0, 1.0, 0.2)
+    G, WD, Y, Rr = gz.cuda().to(dt), wd.cuda().to(dt), y.cuda().to(dt), r.cuda().contiguous()
+    out = torch.zeros(B, H, H, C, dtype=dt, device="cuda")
+    hip.conv3x3(G, WD, out, B=B, H=H, W=H, cin=C, cout=C, flags=CONV_PNBWD, aux=Y, y2=Rr)
+    gy = torch.zeros(B, H, H, C, dtype=dt, device="cuda")
+    hip.conv3x3(G, WD, gy, B=B, H=H, W=H, cin=C, cout=C, flags=0)
+    unf = torch.zeros_like(gy)
+    hip.pixnorm_lrelu_bwd_y(Y, Rr, gy, unf, C, 0.2)
+    torch.cuda.synchronize()
+    cmp(out, ref, 1e-2, f"fused PNBWD H={H} C={C}")
+    cmp(out, unf.float().cpu(), 2e-2, f"fused vs unfused H={H} C={C}")
