@@ -19,7 +19,7 @@ for step in "$@"; do
     parity) run parity 1200 python -m pytest tests/test_gpu_parity.py -q ;;
     gpu) run gpu 1500 python -m pytest tests -q -m gpu ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) run bench 900 python bench.py --steps 5 --warmup 2 ;;
+    bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
     prof)
       ROOT=$(pwd)
