@@ -1323,10 +1323,24 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const pg_pack_item* ite
   const int o0 = (blockIdx.x / tc) * 32, c0 = (blockIdx.x % tc) * 32;
   __shared__ float s[32][32 * 9 + 1];
   const int tid = threadIdx.x;
-  for (int i = tid; i < 32 * 288; i += 256) {
-    const int ol = i / 288, j = i - ol * 288;
-    const int o = o0 + ol, c = c0 + j / 9;
-    s[ol][j] = (o < cout && c < cin) ? it.w[((size_t)o * cin + c0) * 9 + j] * it.scale : 0.f;
+  if ((cin & 3) == 0 && ((uintptr_t)it.w & 15) == 0) {
+    // 16-byte loads: a row segment (o, c0..c0+31) is 288 contiguous floats at a multiple of 4
+#pragma unroll 3
+    for (int i = tid; i < 32 * 72; i += 256) {
+      const int ol = i / 72, j = (i - ol * 72) * 4;
+      const int o = o0 + ol;
+      f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (o < cout && c0 + j / 9 < cin)   // cin % 4 == 0: a 4-group never straddles cin
+        v = *reinterpret_cast<const f32x4_t*>(it.w + ((size_t)o * cin + c0) * 9 + j);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[ol][j + k] = (c0 + (j + k) / 9 < cin) ? v[k] * it.scale : 0.f;
+    }
+  } else {
+    for (int i = tid; i < 32 * 288; i += 256) {
+      const int ol = i / 288, j = i - ol * 288;
+      const int o = o0 + ol, c = c0 + j / 9;
+      s[ol][j] = (o < cout && c < cin) ? it.w[((size_t)o * cin + c0) * 9 + j] * it.scale : 0.f;
+    }
   }
   __syncthreads();
   T* fwd = reinterpret_cast<T*>(it.fwd);
