@@ -991,10 +991,32 @@ __global__ void r1_kernel(int B, size_t n, const float* g, float* r1, float* gba
   __shared__ float red[16];
   float part = 0.f;
   const float inv = 1.f / (float)B;
-  GRID_STRIDE(i, n) {
-    const float v = g[i];
-    part += v * v;
-    if (gbar) gbar[i] = v * inv;
+  if ((n & 3) == 0 && (((uintptr_t)g | (uintptr_t)gbar) & 15) == 0) {
+    // 16-byte accesses, two vectors in flight per thread
+    const size_t n4 = n >> 2, stride = (size_t)gridDim.x * blockDim.x;
+    const f32x4_t* g4 = reinterpret_cast<const f32x4_t*>(g);
+    f32x4_t* b4 = reinterpret_cast<f32x4_t*>(gbar);
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + stride < n4; i += 2 * stride) {
+      const f32x4_t v0 = g4[i], v1 = g4[i + stride];
+      part += v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2] + v0[3] * v0[3];
+      part += v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2] + v1[3] * v1[3];
+      if (gbar) {
+        b4[i] = v0 * inv;
+        b4[i + stride] = v1 * inv;
+      }
+    }
+    for (; i < n4; i += stride) {
+      const f32x4_t v0 = g4[i];
+      part += v0[0] * v0[0] + v0[1] * v0[1] + v0[2] * v0[2] + v0[3] * v0[3];
+      if (gbar) b4[i] = v0 * inv;
+    }
+  } else {
+    GRID_STRIDE(i, n) {
+      const float v = g[i];
+      part += v * v;
+      if (gbar) gbar[i] = v * inv;
+    }
   }
   const float t = block_sum(part, red);
   if (threadIdx.x == 0) atomicAdd(r1, 0.5f * t * inv);
