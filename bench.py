@@ -167,8 +167,14 @@ def pmc_traffic(args, fam):
     separate --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, gfx950 FETCH x2 correction).
     PMC counters cannot be read inside the timed run, so this is the profiled twin's value."""
     import glob
+    import re
     key = f"stage{args.stage}_b{args.batch}_{args.dtype}"
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_prof_summary.json")), reverse=True):
+
+    def version(path):   # r<round>_v<n>: numeric order (r1_v10 is newer than r1_v9)
+        return tuple(int(t) for t in re.findall(r"\d+", os.path.basename(path)))
+
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_prof_summary.json")), key=version,
+                    reverse=True):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
