@@ -8,9 +8,10 @@ random-init weights (reference init: W ~ N(0,1), b = 0).
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
          (N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
-One process per GPU; gradients all-reduced (mean) over RCCL before each Adam step, the
-exchange overlapped with the work that does not depend on it (engine.train_step).
-Rank 0 prints ONE JSON line.
+The timed step is ProgressiveGAN.train_step (the path train.py runs).  One process per
+GPU; gradients all-reduced (mean) over RCCL in per-layer buckets as the backward
+finishes them (pggan_amd.dp), overlapped with the work that does not depend on them
+(engine.train_step).  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -32,6 +33,7 @@ PEAK_HBM_GBS = 8000.0
 # minimal algorithmic GFLOP per image of the step (counted over the reference's
 # own train_step incl. the double backward, without the discarded D wgrad of the G half)
 STEP_GFLOP_PER_IMG = {5: 626.63, 6: 844.33, 7: 1062.29, 8: 1280.78}
+CONFIG_NAME = {(5, 16): "C2", (6, 8): "C3", (7, 8): "C4", (8, 4): "C5"}
 
 
 def parse():
@@ -44,7 +46,8 @@ def parse():
     p.add_argument("--alpha", type=float, default=1.0)
     p.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: os.cpu_count()")
+    p.add_argument("--gp-mode", choices=["r1", "wgan-gp"], default="r1")
     p.add_argument("--no-kernel-events", action="store_true")
     return p.parse_args()
 
@@ -133,32 +136,59 @@ class KernelTimer:
         # the f32 path and the f32-MFMA wgrad kernel run at the f32 MFMA rate
         return "f32" if self.dtype == "f32" else "bf16"
 
-    def summary(self):
-        out = {}
-        for k, lst in self.rec.items():
-            if not lst:
-                continue
-            pf = PEAK_TFLOPS[self.peak_key(k)] * 1e12
-            ms = sum(a.elapsed_time(b) for a, b, _, _ in lst)
-            fl = sum(f for _, _, f, _ in lst)
-            by = sum(v for _, _, _, v in lst)
-            # per-launch roofline time: max(flops / MFMA peak, bytes / HBM peak)
-            roof_s = sum(max(f / pf, v / (PEAK_HBM_GBS * 1e9)) for _, _, f, v in lst)
-            out[k] = dict(launches=len(lst), total_ms=ms, avg_us=1e3 * ms / len(lst),
-                          flops=fl, bytes=by, tflops=fl / (ms * 1e-3) / 1e12,
-                          gbps=by / (ms * 1e-3) / 1e9, roofline_time_frac=roof_s / (ms * 1e-3),
-                          t_mfma_s=fl / pf, t_hbm_s=by / (PEAK_HBM_GBS * 1e9))
+    def _launches(self):
+        """(family, H, flops, bytes, ms, bound) per recorded launch; bound = the roofline
+        that limits THIS launch: mfma if flops/peak >= bytes/HBM peak, else hbm."""
+        pf = PEAK_TFLOPS[self.peak_key("")] * 1e12
+        out = []
+        for fam, H, ci, co, fl, a, b, f, by in self.shapes:
+            bound = "mfma" if f / pf >= by / (PEAK_HBM_GBS * 1e9) else "hbm"
+            out.append((fam, H, f, by, a.elapsed_time(b), bound))
         return out
 
+    def summary(self):
+        """Per (family, bound) group: launches, time, FLOPs, bytes, achieved rates, and the
+        per-launch roofline fraction sum(max(t_mfma, t_hbm)) / sum(t)."""
+        pf = PEAK_TFLOPS[self.peak_key("")] * 1e12
+        groups = {}
+        for fam, H, f, by, ms, bound in self._launches():
+            g = groups.setdefault(f"{fam}/{bound}", dict(launches=0, total_ms=0.0, flops=0.0,
+                                                         bytes=0.0, roof_s=0.0, bound=bound))
+            g["launches"] += 1
+            g["total_ms"] += ms
+            g["flops"] += f
+            g["bytes"] += by
+            g["roof_s"] += max(f / pf, by / (PEAK_HBM_GBS * 1e9))
+        for g in groups.values():
+            t = g["total_ms"] * 1e-3
+            g.update(avg_us=1e3 * g["total_ms"] / g["launches"], tflops=g["flops"] / t / 1e12,
+                     gbps=g["bytes"] / t / 1e9, roofline_time_frac=g["roof_s"] / t)
+        return groups
 
-def init_params(E, depths, s, device, rank_seed):
-    gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
-    gen = torch.Generator().manual_seed(1234)   # same init on every rank (then broadcast)
-    init = lambda sh: {k: (torch.randn(v, generator=gen) if k.endswith("weight")
-                           else torch.zeros(v)) for k, v in sh}
-    fpG = E.FlatParams(gsh, E.dead_params("G", s), device, init(gsh))
-    fpD = E.FlatParams(dsh, E.dead_params("D", s), device, init(dsh))
-    return fpG, fpD
+    def per_resolution(self):
+        """The north star's view: per resolution of the conv / weight-gradient launches,
+        achieved TFLOP/s and MFMA fraction, achieved GB/s and HBM fraction, and which
+        roofline bounds the majority of that resolution's launch time."""
+        pf = PEAK_TFLOPS[self.peak_key("")] * 1e12
+        rows = {}
+        for fam, H, f, by, ms, bound in self._launches():
+            r = rows.setdefault(H, dict(ms=0.0, flops=0.0, bytes=0.0, ms_mfma=0.0, launches=0))
+            r["ms"] += ms
+            r["flops"] += f
+            r["bytes"] += by
+            r["launches"] += 1
+            if bound == "mfma":
+                r["ms_mfma"] += ms
+        out = []
+        for H in sorted(rows):
+            r = rows[H]
+            t = r["ms"] * 1e-3
+            tf, gb = r["flops"] / t / 1e12, r["bytes"] / t / 1e9
+            out.append(dict(res=H, launches=r["launches"], ms_per_step=round(r["ms"], 3),
+                            bound="mfma" if r["ms_mfma"] >= 0.5 * r["ms"] else "hbm",
+                            tflops=round(tf, 1), mfma_frac=round(tf * 1e12 / pf, 4),
+                            gbps=round(gb, 1), hbm_frac=round(gb / PEAK_HBM_GBS, 4)))
+        return out
 
 
 def pmc_traffic(args, fam):
@@ -179,7 +209,7 @@ def pmc_traffic(args, fam):
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        f = d.get("families", {}).get(fam, {})
+        f = d.get("groups", {}).get(fam, {})
         if d.get("config") == key and f.get("hbm_bytes_per_call"):
             return round(f["hbm_bytes_per_call"]), os.path.relpath(p, ROOT)
     return None, None
@@ -187,9 +217,11 @@ def pmc_traffic(args, fam):
 
 def cpu_baseline(args, steps=1):
     """The CPU oracle (fp32 restatement of the reference step, pinned to the reference's
-    golden vectors) on the host cores: one train_step at the same workload."""
+    golden vectors) on the host cores: one train_step at the same workload, with
+    torch.set_num_threads(os.cpu_count()) (CPU-baseline plan)."""
     from oracle import pggan_oracle as O
-    torch.set_num_threads(args.cpu_threads)
+    threads = args.cpu_threads or os.cpu_count() or 1
+    torch.set_num_threads(threads)
     s, B = args.stage, args.batch
     depths = PAPER_DEPTHS
     gen = torch.Generator().manual_seed(7)
@@ -206,9 +238,38 @@ def cpu_baseline(args, steps=1):
         z2 = torch.randn(B, 512, generator=gen)
         O.train_step(PG, PD, optG, optD, real, z1, z2, s, args.alpha, args.alpha)
     dt = time.perf_counter() - t0
-    return dict(value=B * steps / dt, unit="images/sec", cores=args.cpu_threads, kind="port",
+    return dict(value=B * steps / dt, unit="images/sec", cores=threads, kind="port",
+                host_cpu_count=os.cpu_count(),
                 sample=f"{steps} oracle train_step at {R}x{R}, batch {B}, alpha {args.alpha} "
-                       f"(fp32, torch CPU, {args.cpu_threads} threads): {dt:.1f} s")
+                       f"(fp32, torch CPU, torch.set_num_threads({threads})): {dt:.1f} s")
+
+
+def build_model(args, rank, local, world, ops_factory):
+    """The product path train.py runs: ProgressiveGAN (pggan/model.py:11-265 interface)
+    grown to the benchmark stage, reference init (W ~ N(0,1), b = 0), the resident
+    synthetic batch (`synthetic_data`), RCCL gradient exchange when world > 1."""
+    from pggan_amd.config import Config
+    from pggan_amd.model import ProgressiveGAN
+    cfg = Config.from_yaml(os.path.join(ROOT, "pggan_amd", "default_config.yaml"))
+    cfg.update(depths=list(PAPER_DEPTHS), batch_per_gpu=args.batch, compute_dtype=args.dtype,
+               synthetic_data=True, isMaster=False, use_mGPU=world > 1, gpu_num=world,
+               run_id="bench", gp_mode=args.gp_mode)
+    ProgressiveGAN.ops_factory = ops_factory
+    torch.manual_seed(1234)                      # same init on every rank (then broadcast)
+    m = ProgressiveGAN(cfg, local)
+    m.initialize_models()
+    for i in range(1, args.stage + 1):           # pggan/model.py:158-169 add_block per stage
+        m.G.add_block(PAPER_DEPTHS[i])
+        m.D.add_block(PAPER_DEPTHS[i])
+    m.scale_index = args.stage
+    m.G.alpha = m.D.alpha = args.alpha
+    if world > 1:
+        m.set_multi_GPU()                        # RCCL, parameter broadcast, GradExchange
+    m.set_optimizers()
+    m.set_dataset()
+    m.set_data_iterator()
+    m.set_loss_collector()
+    return m
 
 
 def main():
@@ -232,7 +293,6 @@ def main():
             dist.init_process_group(backend)
 
     from pggan_amd import _lib
-    from pggan_amd import engine as E
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     ops = _lib.HipOps(dtype)
@@ -240,41 +300,14 @@ def main():
     s, B = args.stage, args.batch
     depths = PAPER_DEPTHS
     R = 4 * 2 ** s
-    fpG, fpD = init_params(E, depths, s, dev, rank)
-    if world > 1:   # replaces DDP's constructor-time broadcast (lib/model.py:78-79)
-        dist.broadcast(fpG.flat, 0)
-        dist.broadcast(fpD.flat, 0)
-    eng = E.StepEngine(ops, depths, s, B, dev)
-    eng.bind(fpG, fpD, E.Hyper())
-    gen = torch.Generator(device=dev).manual_seed(1000 * rank)
-    real = torch.rand(B, 3, R, R, device=dev, generator=gen) * 2 - 1
-    z = torch.empty(2, B, 512, device=dev)
-
-    class Pending:
-        """Async RCCL all-reduce of a net's flat live gradient; the engine waits (and the
-        mean is applied) right before that net's Adam step, so the exchange overlaps the
-        work that does not depend on it (engine.train_step)."""
-
-        def __init__(self, g):
-            self.g, self.work = g, dist.all_reduce(g, async_op=True)
-
-        def wait(self):
-            self.work.wait()
-            self.g.mul_(1.0 / world)
-
-    def hook(net, g):
-        return Pending(g) if world > 1 else None
-
-    step_no = [0]
+    model = build_model(args, rank, local, world, lambda dt: ops)
 
     def step():
-        ops.randn(z, 1000 * rank + 17, step_no[0] * z.numel())
-        step_no[0] += 1
-        eng.train_step(real, z[0], z[1], args.alpha, args.alpha, grad_hook=hook)
+        model.train_step()
 
     for _ in range(args.warmup):
         step()
-    eng.flush()
+    model.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -287,7 +320,7 @@ def main():
         if timer:
             timer.on = i == args.steps - 1
         step()
-    eng.flush()          # the last step's (deferred) generator update is part of the step
+    model.flush()        # the last step's (deferred) generator update is part of the step
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -300,14 +333,15 @@ def main():
     h0 = time.perf_counter()
     for _ in range(2):
         step()
-    eng.flush()
+    model.flush()
     host_ms = (time.perf_counter() - h0) * 1e3 / 2
     torch.cuda.synchronize()
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    assert torch.isfinite(eng.loss).all(), "non-finite loss"
+    ld = model.loss_collector.loss_dict
+    assert all(v == v and abs(v) != float("inf") for v in ld.values()), f"non-finite loss {ld}"
     ksum = timer.summary() if timer else {}
     if timer and os.environ.get("PG_BENCH_SHAPES"):
         with open(os.environ["PG_BENCH_SHAPES"], "w") as f:
@@ -316,15 +350,18 @@ def main():
     if rank == 0:
         roof = None
         if ksum:
+            # dominant = the (kernel family, bound) group with the most time: every launch
+            # is classified against its own roofline, so a group's achieved rate and peak
+            # are in the same unit
             dom = max(ksum, key=lambda k: ksum[k]["total_ms"])
             kd = ksum[dom]
-            hbm = kd["t_hbm_s"] > kd["t_mfma_s"]
-            if hbm:
+            fam = dom.split("/")[0]
+            if kd["bound"] == "hbm":
                 ach, peak, unit = kd["gbps"], PEAK_HBM_GBS, "GB/s"
             else:
-                ach, peak, unit = kd["tflops"], PEAK_TFLOPS[timer.peak_key(dom)], "TFLOP/s"
+                ach, peak, unit = kd["tflops"], PEAK_TFLOPS[timer.peak_key(fam)], "TFLOP/s"
             traffic, tsrc = pmc_traffic(args, dom)
-            roof = dict(bound="hbm" if hbm else "mfma", kernel=dom, achieved=round(ach, 2),
+            roof = dict(bound=kd["bound"], kernel=dom, achieved=round(ach, 2),
                         peak=peak, unit=unit, frac=round(ach / peak, 4), traffic=traffic,
                         traffic_source=tsrc,
                         algorithmic_bytes_per_launch=round(kd["bytes"] / kd["launches"]),
@@ -333,15 +370,16 @@ def main():
                         avg_launch_us=round(kd["avg_us"], 2),
                         roofline_time_frac=round(kd["roofline_time_frac"], 4),
                         # whole-step MFMA fraction at the minimal algorithmic
-                        # 1280.78 GFLOP per image (C5), all kernels, wall clock
+                        # GFLOP per image (1280.78 at C5), all kernels, wall clock
                         step_mfma_frac=round(STEP_GFLOP_PER_IMG.get(args.stage, 0.0) * 1e9 *
                                              B * args.steps / dt /
                                              (PEAK_TFLOPS[args.dtype] * 1e12), 4),
-                        kernels={k: dict(total_ms_per_step=round(v["total_ms"], 3),
-                                         tflops=round(v["tflops"], 2), gbps=round(v["gbps"], 1),
-                                         roofline_time_frac=round(v["roofline_time_frac"], 4),
-                                         launches_per_step=v["launches"])
-                                 for k, v in ksum.items()})
+                        groups={k: dict(total_ms_per_step=round(v["total_ms"], 3),
+                                        tflops=round(v["tflops"], 2), gbps=round(v["gbps"], 1),
+                                        roofline_time_frac=round(v["roofline_time_frac"], 4),
+                                        launches_per_step=v["launches"])
+                                for k, v in sorted(ksum.items())},
+                        per_resolution=timer.per_resolution())
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             cpu = cpu_baseline(args)
@@ -359,8 +397,10 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic (U[-1,1) reals resident in HBM, N(0,1) latents on GPU, "
                     "random-init weights)",
-            "config": {"workload": f"C5 G+D+R1 train_step, stage {s} ({R}x{R}), batch {B}/GPU, "
-                                   f"alpha {args.alpha}, depths {depths}",
+            "config": {"workload": f"{CONFIG_NAME.get((s, B), 'custom')} G+D+"
+                                   f"{'R1' if args.gp_mode == 'r1' else 'WGAN-GP'} train_step "
+                                   f"via ProgressiveGAN.train_step, stage {s} ({R}x{R}), "
+                                   f"batch {B}/GPU, alpha {args.alpha}, depths {depths}",
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
             "host_enqueue_ms_per_step": round(host_ms, 3),

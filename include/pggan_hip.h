@@ -239,6 +239,9 @@ int pg_mbstd_r1(int dtype, int B, int HW, int C, int x_cs, const void* x, const 
  * h = d u / d l (for the R1 double-backward).  loss_out[0] += w * loss. */
 int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out, float* u,
                 float* h, void* stream);
+/* WGAN-GP mode drift term (pggan/loss.py:94-100 get_drift_loss): loss_out[0] += w * sum_b l_b^2
+ * and u_b += 2 w l_b (u: the logit gradient of the real-image BCE, accumulated) */
+int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u, void* stream);
 /* R1 = 0.5 * mean_b sum g^2 accumulated into r1_out[0]; gbar = g / B  (g: [n] fp32, B samples) */
 int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream);
 /* WGAN-GP optional mode (pggan/loss.py:54-92): interp = eps*xr + (1-eps)*xf (per-sample eps) */

@@ -56,6 +56,52 @@ def lrelu(x, slope=0.2):
     return F.leaky_relu(x, slope)
 
 
+class Kinks:
+    """Leaky-ReLU region choices injected from another implementation's forward pass.
+
+    Parity tests only.  A pre-activation within rounding of 0 can take the other slope
+    under any change of summation order, and its gradient then changes by 1/slope; with
+    10^5-10^7 pre-activations per layer such flips are expected between two correct
+    implementations.  Injecting the region choice of the implementation under test makes
+    both compute the same piecewise-linear function, so the remaining difference is pure
+    rounding and every tensor can be held to the strict bar.  Each site records how many
+    elements the injected choice flips relative to this forward's own sign, and the
+    largest |pre-activation| among them relative to the site's RMS: the tests assert that
+    bound, so a real kernel error (a wrong sign far from 0) cannot hide behind a mask.
+
+    masks: {site: bool tensor shaped like the pre-activation (NCHW / [B, N])}, True =
+    slope 1.  Every site the forward reaches must be present."""
+
+    def __init__(self, masks):
+        self.masks = masks
+        self.stats = {}
+
+    def act(self, x, site, slope):
+        m = self.masks[site].to(x.device)
+        assert m.shape == x.shape, (site, tuple(m.shape), tuple(x.shape))
+        with torch.no_grad():
+            own = x > 0
+            flip = own != m
+            n = int(flip.sum())
+            rms = float(x.detach().double().pow(2).mean().sqrt()) or 1.0
+            worst = float(x.detach()[flip].abs().max()) / rms if n else 0.0
+            self.stats[site] = (n, x.numel(), worst)
+        k = torch.where(m, torch.ones((), dtype=x.dtype), torch.full((), slope, dtype=x.dtype))
+        return x * k
+
+    def flips(self):
+        return sum(v[0] for v in self.stats.values())
+
+    def worst(self):
+        return max((v[2] for v in self.stats.values()), default=0.0)
+
+
+def _act(kinks):
+    if kinks is None:
+        return lambda x, site, slope: lrelu(x, slope)
+    return kinks.act
+
+
 def upscale2d(x):
     """lib/utils.py:106-118 nearest x2 via view/expand."""
     s = x.shape
@@ -135,16 +181,19 @@ def d_param_shapes(depths, s, in_dim=3):
     return shapes
 
 
-def generator_forward(P, z, s, alpha, slope_cfg=0.2):
-    """pggan/nets.py:121-161 Generator.forward."""
+def generator_forward(P, z, s, alpha, slope_cfg=0.2, kinks=None):
+    """pggan/nets.py:121-161 Generator.forward.  kinks: optional Kinks (parity tests)
+    with sites fmt, first, a{i}, b{i}."""
+    act = _act(kinks)
     x = pixel_norm(z)                                              # :124-125
     x = x.view(-1, x[0].numel())                                   # :126
-    x = lrelu(eq_linear(x, P["latent_format_layer.module.weight"],
-                        P["latent_format_layer.module.bias"]), slope_cfg)   # :129
+    x = act(eq_linear(x, P["latent_format_layer.module.weight"],
+                      P["latent_format_layer.module.bias"]), "fmt", slope_cfg)   # :129
     x = x.view(x.shape[0], -1, 4, 4)                               # :130
     x = pixel_norm(x)                                              # :132-133
-    x = pixel_norm(lrelu(eq_conv(x, P["first_block.block.0.module.weight"],
-                                 P["first_block.block.0.module.bias"], 1)))  # :136, blocks.py:131-139
+    x = pixel_norm(act(eq_conv(x, P["first_block.block.0.module.weight"],
+                               P["first_block.block.0.module.bias"], 1), "first", 0.2))
+    # :136, blocks.py:131-139
 
     def to_rgb(i, h, up):                                          # blocks.py:153-170
         y = eq_conv(h, P[f"toRGB_blocks.{i}.toRGB.module.weight"],
@@ -156,10 +205,10 @@ def generator_forward(P, z, s, alpha, slope_cfg=0.2):
         x_up = to_rgb(s - 1, x, True)                              # :140-141
     for i in range(s):                                             # :144-149
         x = upscale2d(x)
-        x = pixel_norm(lrelu(eq_conv(x, P[f"blocks.{i}.block.0.module.weight"],
-                                     P[f"blocks.{i}.block.0.module.bias"], 1)))
-        x = pixel_norm(lrelu(eq_conv(x, P[f"blocks.{i}.block.3.module.weight"],
-                                     P[f"blocks.{i}.block.3.module.bias"], 1)))
+        x = pixel_norm(act(eq_conv(x, P[f"blocks.{i}.block.0.module.weight"],
+                                   P[f"blocks.{i}.block.0.module.bias"], 1), f"a{i}", 0.2))
+        x = pixel_norm(act(eq_conv(x, P[f"blocks.{i}.block.3.module.weight"],
+                                   P[f"blocks.{i}.block.3.module.bias"], 1), f"b{i}", 0.2))
         if i == s - 2:
             x_up = to_rgb(s - 1, x, True)
     x = to_rgb(s, x, False)                                        # :152
@@ -168,32 +217,35 @@ def generator_forward(P, z, s, alpha, slope_cfg=0.2):
     return x
 
 
-def discriminator_forward(P, x, s, alpha, get_feature=False):
-    """pggan/nets.py:248-276 Discriminator.forward."""
-    def from_rgb(i, h, down):                                      # blocks.py:271-292
+def discriminator_forward(P, x, s, alpha, get_feature=False, kinks=None):
+    """pggan/nets.py:248-276 Discriminator.forward.  kinks: optional Kinks (parity tests)
+    with sites rgb, rgbd, a{i}, b{i}, mb, lin."""
+    act = _act(kinks)
+
+    def from_rgb(i, h, down, site):                                # blocks.py:271-292
         if down:
             h = downscale2d(h)
-        return lrelu(eq_conv(h, P[f"fromRGB_blocks.{i}.fromRGB.module.weight"],
-                             P[f"fromRGB_blocks.{i}.fromRGB.module.bias"], 0))
+        return act(eq_conv(h, P[f"fromRGB_blocks.{i}.fromRGB.module.weight"],
+                           P[f"fromRGB_blocks.{i}.fromRGB.module.bias"], 0), site, 0.2)
 
-    x_down = from_rgb(s - 1, x, True) if s else None               # :251-252
-    x = from_rgb(s, x, False)                                      # :255
+    x_down = from_rgb(s - 1, x, True, "rgbd") if s else None       # :251-252
+    x = from_rgb(s, x, False, "rgb")                               # :255
     merge = s > 0
     for i in reversed(range(s)):                                   # :260-265, blocks.py:179-199
-        x = lrelu(eq_conv(x, P[f"blocks.{i}.block.0.module.weight"],
-                          P[f"blocks.{i}.block.0.module.bias"], 1))
-        x = lrelu(eq_conv(x, P[f"blocks.{i}.block.2.module.weight"],
-                          P[f"blocks.{i}.block.2.module.bias"], 1))
+        x = act(eq_conv(x, P[f"blocks.{i}.block.0.module.weight"],
+                        P[f"blocks.{i}.block.0.module.bias"], 1), f"a{i}", 0.2)
+        x = act(eq_conv(x, P[f"blocks.{i}.block.2.module.weight"],
+                        P[f"blocks.{i}.block.2.module.bias"], 1), f"b{i}", 0.2)
         x = F.avg_pool2d(x, (2, 2))
         if merge:
             merge = False
             x = (1 - alpha) * x_down + alpha * x
     x = mbstd(x)                                                   # blocks.py:261
-    x = lrelu(eq_conv(x, P["minibatch_normalization_block.conv.module.weight"],
-                      P["minibatch_normalization_block.conv.module.bias"], 1))
+    x = act(eq_conv(x, P["minibatch_normalization_block.conv.module.weight"],
+                    P["minibatch_normalization_block.conv.module.bias"], 1), "mb", 0.2)
     x = x.view(-1, x[0].numel())
-    x = lrelu(eq_linear(x, P["minibatch_normalization_block.linear.module.weight"],
-                        P["minibatch_normalization_block.linear.module.bias"]))
+    x = act(eq_linear(x, P["minibatch_normalization_block.linear.module.weight"],
+                      P["minibatch_normalization_block.linear.module.bias"]), "lin", 0.2)
     out = eq_linear(x, P["decision_layer.module.weight"], P["decision_layer.module.bias"])
     return (out, x) if get_feature else out
 
@@ -215,7 +267,8 @@ def r1_reg(d_out, x_in):
 
 def wgan_gp(Dfn, img_real, img_fake, eps, w_gp):
     """pggan/loss.py:54-92 get_gradient_penalty (dead in the reference; optional mode).
-    eps: [B,1] uniform; sum over batch of (||grad||-1)^2 times W_gp."""
+    eps: [B,1] uniform (:71-73); x^ = eps*x_r + (1-eps)*x_f (:75); d = sum_b D(x^)[:,0]
+    (:78-79); per-sample L2 norm of dd/dx^ (:81-86); W_gp * sum_b (|g|-1)^2 (:87)."""
     B = img_real.shape[0]
     e = eps.expand(B, img_real[0].numel()).contiguous().view(img_real.shape)
     interp = (e * img_real + (1 - e) * img_fake).detach().requires_grad_()
@@ -224,6 +277,11 @@ def wgan_gp(Dfn, img_real, img_fake, eps, w_gp):
     g = g.view(B, -1)
     g = (g * g).sum(dim=1).sqrt()
     return ((g - 1.0) ** 2).sum() * w_gp
+
+
+def drift_loss(pred_real, w_drift):
+    """pggan/loss.py:94-100 get_drift_loss: W_drift_D * sum_b D(x_real)^2."""
+    return (pred_real ** 2).sum() * w_drift
 
 
 # --------------------------------------------------------------------------
@@ -277,16 +335,36 @@ class StepOut:
     L_G: float
     grads_D: dict
     grads_G: dict
+    drift: float = 0.0
 
 
 def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
-               W_adv=1.0, slope_cfg=0.2, gp_mode="r1", gp_eps=None, W_gp=10.0):
+               W_adv=1.0, slope_cfg=0.2, gp_mode="r1", gp_eps=None, W_gp=10.0, W_drift=0.0,
+               kinks=None, fake_D=None, fake_G=None):
     """pggan/model.py:206-255 ProgressiveGAN.train_step on CPU; updates PG/PD in place.
 
     gp_mode="r1" is the live reference path (pggan/loss.py:16-27).
-    gp_mode="wgan-gp" adds the dead get_gradient_penalty term instead of R1
-    (pggan/loss.py:54-92), an optional mode the north star names.
-    """
+    gp_mode="wgan-gp" is the optional mode the north star names: L_D = BCE(real,1) +
+    BCE(fake,0) + get_gradient_penalty (pggan/loss.py:54-92) + get_drift_loss
+    (:94-100), both terms differentiated into D's gradient (the paper's meaning; the
+    reference's code for them is never called).
+
+    kinks: optional {"D": [Kinks...], "G": [Kinks...]} consumed in forward-call order
+    (D: real, fake, [interpolate], fake of the G half; G: z1, z2) -- parity tests only.
+    fake_D / fake_G: optional fake images of the implementation under test, fed to D in
+    place of this G's output (parity tests, to compare each network on identical inputs;
+    the G half keeps this G's gradient path: the value is fake_G, the gradient flows
+    into this G).  The returned img_fake_* are always this G's own outputs.
+    Works in any floating dtype (the tests run it in float64)."""
+    kD = list(kinks["D"]) if kinks else []
+    kG = list(kinks["G"]) if kinks else []
+
+    def D(P, x, get_feature=False):
+        return discriminator_forward(P, x, s, alpha_D, get_feature, kD.pop(0) if kinks else None)
+
+    def G(P, z):
+        return generator_forward(P, z, s, alpha_G, slope_cfg, kG.pop(0) if kinks else None)
+
     for P in (PG, PD):
         for k in P:
             P[k].requires_grad_(True)
@@ -294,25 +372,32 @@ def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
         low = F.interpolate(F.avg_pool2d(img_real, (2, 2)), scale_factor=2, mode="nearest")
         img_real = (1 - alpha_D) * low + alpha_D * img_real
     img_real = img_real.detach().clone().requires_grad_()          # :223
-    pred_real = discriminator_forward(PD, img_real, s, alpha_D)     # :224
-    img_fake = generator_forward(PG, z1, s, alpha_G, slope_cfg).detach()   # :226-227
-    pred_fake = discriminator_forward(PD, img_fake, s, alpha_D)     # :228
+    pred_real = D(PD, img_real)                                     # :224
+    img_fake = G(PG, z1).detach()                                   # :226-227
+    img_fake_own = img_fake
+    if fake_D is not None:
+        img_fake = fake_D.detach().to(img_fake.dtype)
+    pred_fake = D(PD, img_fake)                                     # :228
     L_real = bce_logits(pred_real, 1)                               # pggan/loss.py:18-21
     L_fake = bce_logits(pred_fake, 0)
+    drift = None
     if gp_mode == "r1":
         reg = r1_reg(L_real, img_real)
     else:
-        reg = wgan_gp(lambda t: discriminator_forward(PD, t, s, alpha_D), img_real.detach(),
-                      img_fake, gp_eps, W_gp)
-    L_D = L_real + L_fake + reg
+        reg = wgan_gp(lambda t: D(PD, t), img_real.detach(), img_fake, gp_eps, W_gp)
+        drift = drift_loss(pred_real, W_drift)
+    L_D = L_real + L_fake + reg + (drift if drift is not None else 0.0)
     dkeys = list(PD.keys())
     gd = torch.autograd.grad(L_D, [PD[k] for k in dkeys], allow_unused=True)
     grads_D = dict(zip(dkeys, gd))
     with torch.no_grad():
         optD.update(PD, grads_D)                                    # lib/utils.py:72-75
 
-    img_fake_G = generator_forward(PG, z2, s, alpha_G, slope_cfg)   # :244-245
-    pred_fake_G = discriminator_forward(PD, img_fake_G, s, alpha_D)  # :246
+    img_fake_G = G(PG, z2)                                          # :244-245
+    img_fake_G_own = img_fake_G
+    if fake_G is not None:
+        img_fake_G = img_fake_G + (fake_G.to(img_fake_G.dtype) - img_fake_G).detach()
+    pred_fake_G = D(PD, img_fake_G)                                 # :246
     L_G = W_adv * bce_logits(pred_fake_G, 1)                        # pggan/loss.py:5-14
     gkeys = list(PG.keys())
     gg = torch.autograd.grad(L_G, [PG[k] for k in gkeys], allow_unused=True)
@@ -322,8 +407,9 @@ def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
     for P in (PG, PD):
         for k in P:
             P[k].requires_grad_(False)
-    return StepOut(img_real.detach(), img_fake, img_fake_G.detach(), pred_real.detach(),
+    return StepOut(img_real.detach(), img_fake_own, img_fake_G_own.detach(), pred_real.detach(),
                    pred_fake.detach(), pred_fake_G.detach(), L_real.item(), L_fake.item(),
                    float(reg.detach()) if torch.is_tensor(reg) else float(reg), L_D.item(), L_G.item(),
                    {k: (None if v is None else v.detach()) for k, v in grads_D.items()},
-                   {k: (None if v is None else v.detach()) for k, v in grads_G.items()})
+                   {k: (None if v is None else v.detach()) for k, v in grads_G.items()},
+                   float(drift.detach()) if drift is not None else 0.0)

@@ -96,6 +96,7 @@ _SIGS = {
     "pg_mbstd_r1": ([_I, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP], _I),
     "pg_bce_loss": ([_I, _VP, _I, _F, _VP, _VP, _VP, _VP], _I),
     "pg_r1_penalty": ([_I, _SZ, _VP, _VP, _VP, _VP], _I),
+    "pg_drift_loss": ([_I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_gp_interp": ([_I, _SZ, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_gp_penalty": ([_I, _SZ, _VP, _F, _VP, _VP, _VP, _VP], _I),
     "pg_mul_add": ([_SZ, _VP, _VP, _VP, _VP, _VP], _I),
@@ -380,6 +381,11 @@ class HipOps:
         self._cuda(logits, loss, u, h)
         self._chk(self.lib.pg_bce_loss(logits.numel(), _p(logits), 1 if target else 0, w, _p(loss),
                                        _p(u), _p(h), self._s()), "bce_loss")
+
+    def drift(self, logits, w, loss, u):
+        self._cuda(logits, loss, u)
+        self._chk(self.lib.pg_drift_loss(logits.numel(), _p(logits), w, _p(loss), _p(u), self._s()),
+                  "drift_loss")
 
     def r1_penalty(self, g, B, r1, gbar):
         self._cuda(g, r1, gbar)

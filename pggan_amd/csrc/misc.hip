@@ -987,6 +987,20 @@ __global__ void bce_kernel(int B, const float* l, int target, float w, float* lo
   if (threadIdx.x == 0 && loss) loss[0] += w * t / (float)B;
 }
 
+// drift term of the WGAN-GP mode (pggan/loss.py:94-100): W * sum_b l_b^2, its logit
+// gradient 2 W l_b added into u (the BCE gradient of the same real logits)
+__global__ void drift_kernel(int B, const float* l, float w, float* loss, float* u) {
+  __shared__ float red[16];
+  float part = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float x = l[b];
+    part += x * x;
+    if (u) u[b] += 2.f * w * x;
+  }
+  const float t = block_sum(part, red);
+  if (threadIdx.x == 0 && loss) loss[0] += w * t;
+}
+
 __global__ void r1_kernel(int B, size_t n, const float* g, float* r1, float* gbar) {
   __shared__ float red[16];
   float part = 0.f;
@@ -1597,6 +1611,14 @@ int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out
   PG_CHECK_ARG(logits && B > 0, "bce_loss: bad args");
   hipLaunchKernelGGL(bce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, target, w,
                      loss_out, u, h);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u, void* stream) {
+  PG_CHECK_ARG(logits && B > 0, "drift_loss: bad args");
+  hipLaunchKernelGGL(drift_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, w,
+                     loss_out, u);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

@@ -1,0 +1,117 @@
+"""Data-parallel gradient exchange: one process per GPU, RCCL over xGMI.
+
+The reference wraps its nets in DistributedDataParallel and immediately discards the
+wrapper (lib/model.py:74-79), so its ranks never exchange gradients.  Here the mean
+over ranks of each net's flat live gradient is all-reduced before that net's Adam
+step, in buckets launched as the final backward pass finishes each layer:
+
+* the engine calls `ready(net, names)` right after the last kernel that writes those
+  parameters' gradients (StepEngine.grad_ready), in backward order -- the 512-channel
+  layers near the logit finish first, so their buckets (the bulk of the 92 MB per net
+  at 1024^2) travel while the high-resolution layers are still being differentiated;
+* `finish(net)` launches what is left and returns a Pending whose wait() completes the
+  exchange and applies the 1/world mean; the engine waits right before that net's Adam
+  step, which it schedules after independent work (the G forward for D, the next
+  step's real-image D part for G; engine.train_step).
+
+A collective enqueued on the RCCL stream waits for the compute stream at the time of
+the call, so every bucket sees its finished gradient.  `reduce_dtype=torch.bfloat16`
+halves the bytes on the links (gradients rounded to bf16 before the sum: an opt-in
+trade, the default fp32 keeps the DP contract exact to fp32 rounding).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class Pending:
+    """The in-flight exchange of one net's gradient; wait() finishes it."""
+
+    def __init__(self, works, grad, world, casts):
+        self.works, self.grad, self.world, self.casts = works, grad, world, casts
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        for lo, hi, buf in self.casts:
+            self.grad[lo:hi].copy_(buf)
+        self.grad.mul_(1.0 / self.world)
+
+
+class GradExchange:
+    """Bucketed asynchronous all-reduce (mean) of flat gradients, one instance per
+    process; `bucket_bytes` is the smallest bucket launched on its own (smaller ready
+    ranges are merged and sent with the next one or at finish)."""
+
+    def __init__(self, world=None, bucket_bytes=4 << 20, reduce_dtype=torch.float32, group=None):
+        self.world = world if world is not None else dist.get_world_size(group)
+        self.bucket_bytes = bucket_bytes
+        self.reduce_dtype = reduce_dtype
+        self.group = group
+        self._fp = {}
+        self._state = {}
+
+    def bind(self, net, fp):
+        """fp: the net's engine.FlatParams (live parameters first)."""
+        self._fp[net] = fp
+        self._state[net] = dict(works=[], casts=[], pend=[], pend_elems=0, sent=[])
+
+    def _launch(self, net, lo, hi):
+        st, g = self._state[net], self._fp[net].grad
+        st["sent"].append((lo, hi))
+        if self.reduce_dtype == torch.float32:
+            st["works"].append(dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
+        else:
+            buf = g[lo:hi].to(self.reduce_dtype)
+            st["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
+            st["casts"].append((lo, hi, buf))
+
+    def _launch_merged(self, net, ranges):
+        """One collective per maximal contiguous span of `ranges`."""
+        run = None
+        for lo, hi in sorted(ranges):
+            if run is not None and lo <= run[1]:
+                run = (run[0], max(run[1], hi))
+                continue
+            if run is not None:
+                self._launch(net, *run)
+            run = (lo, hi)
+        if run is not None:
+            self._launch(net, *run)
+
+    def ready(self, net, names):
+        """Gradients of `names` (a layer's weight and bias) are final."""
+        if net not in self._fp:
+            return
+        fp, st = self._fp[net], self._state[net]
+        for n in names:
+            if n in fp.dead:
+                continue
+            lo, hi = fp.spans[n]
+            st["pend"].append((lo, hi))
+            st["pend_elems"] += hi - lo
+        if st["pend_elems"] * 4 >= self.bucket_bytes:
+            self._launch_merged(net, st["pend"])
+            st["pend"], st["pend_elems"] = [], 0
+
+    def finish(self, net):
+        """Launch the rest of `net`'s live gradient (pending buckets, and any live range the
+        engine never reported) and return its Pending."""
+        fp, st = self._fp[net], self._state[net]
+        done = sorted(st["sent"] + st["pend"])
+        rest, pos = list(st["pend"]), 0
+        for lo, hi in done:
+            if lo > pos:
+                rest.append((pos, lo))
+            pos = max(pos, hi)
+        if pos < fp.n_live:
+            rest.append((pos, fp.n_live))
+        self._launch_merged(net, rest)
+        p = Pending(st["works"], fp.grad, self.world, st["casts"])
+        self.bind(net, fp)
+        return p
+
+    def hook(self, net, g):
+        """engine.train_step grad_hook."""
+        return self.finish(net)

@@ -110,11 +110,13 @@ class FlatParams:
         self.names = [n for n, _ in shapes]          # reference order
         # every tensor starts on a 64-byte boundary (vector loads in the kernels); the
         # padding slots stay zero (zero gradient -> Adam leaves them at zero)
-        self.offsets, off = {}, 0
+        self.offsets, self.spans, off = {}, {}, 0
         self.n_live = 0
         for n in order:
             self.offsets[n] = off
-            off += (int(math.prod(shp[n])) + 15) // 16 * 16
+            padded = (int(math.prod(shp[n])) + 15) // 16 * 16
+            self.spans[n] = (off, off + padded)     # incl. the zero padding slots
+            off += padded
             if n not in dead:
                 self.n_live = off
         self.numel = off
@@ -156,6 +158,7 @@ class Hyper:
     slope_cfg: float = 0.2      # LReLU_slope (G format layer only, pggan/nets.py:45,129)
     gp_mode: str = "r1"         # "r1" (live reference path) | "wgan-gp" (optional mode)
     W_gp: float = 10.0
+    W_drift: float = 0.0        # W_drift_D (wgan-gp mode only, pggan/loss.py:94-100)
 
 
 class StepEngine:
@@ -179,6 +182,12 @@ class StepEngine:
         self.fuse_pnbwd = os.environ.get("PG_PNBWD", "1") != "0"
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
+        # trace(net, engine) after every G / D forward, or None: parity tests read the
+        # leaky-ReLU region choices of each forward from the activation buffers
+        self.trace = None
+        # grad_ready(net, names) right after the last kernel writing those gradients in the
+        # final backward pass of a half-step, or None (DP bucketing, pggan_amd.dp)
+        self.grad_ready = None
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -454,6 +463,8 @@ class StepEngine:
                             d[i + 1], d[i + 1], L.CONV_LRELU, keep)
             prev = g[f"yb{i}"]
         self._rgb_out(P, alpha)
+        if self.trace is not None:
+            self.trace("G", self)
         return g["img"]
 
     def _ylvl(self, j):
@@ -481,6 +492,7 @@ class StepEngine:
         pre = f"toRGB_blocks.{s}.toRGB.module."
         ops.rgb_out_bwd(self._ylvl(s), P[pre + "weight"], he(d[s]), gimg, g[f"gy{s}"],
                         GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s], **kw)
+        self._ready("G", pre, *([f"toRGB_blocks.{s - 1}.toRGB.module."] if s >= 1 else []))
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
@@ -489,6 +501,7 @@ class StepEngine:
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
                         d[i + 1],
                         db=GR[b + "bias"])
+            self._ready("G", b)
             if self._pnb_fused(Ri, d[i], d[i + 1]):
                 # conv b's input gradient with conv a's PixelNorm + LReLU backward in its
                 # epilogue (the gradient w.r.t. ya never goes through HBM)
@@ -502,6 +515,7 @@ class StepEngine:
             self._wgrad("G", f"a{i}", self._ylvl(i), g[f"gza{i}"], GR[a + "weight"], Ri, d[i],
                         d[i + 1], ups=True,
                         db=GR[a + "bias"])
+            self._ready("G", a)
             flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and s >= 1) else 0)
             self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
                        dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
@@ -510,11 +524,13 @@ class StepEngine:
                        L.CONV_LRELU)
         self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
                     db=GR[fb + "bias"])
+        self._ready("G", fb)
         self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)
         ops.pixnorm_lrelu_bwd(g["f"], g["gh0"], g["gzf"], d[0], self.hyper.slope_cfg)
         ops.linear_wgrad(g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
                          GR["latent_format_layer.module.bias"], B=B, flags=L.LIN_OUT_CHW,
                          scale=he(self.latent))
+        self._ready("G", "latent_format_layer.module.")
 
     # ================================================================== D
     def d_forward(self, P, img, alpha):
@@ -549,22 +565,32 @@ class StepEngine:
                    flags=L.LIN_BIAS | L.LIN_LRELU | L.LIN_IN_CHW, scale=he(16 * d[0]), slope=SLOPE)
         ops.linear(D["l1"], P["decision_layer.module.weight"], P["decision_layer.module.bias"],
                    D["logit"], B=B, flags=L.LIN_BIAS, scale=he(d[0]))          # nets.py:271
+        if self.trace is not None:
+            self.trace("D", self)
         return D["logit"]
 
-    def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None):
+    def _ready(self, net, *prefixes):
+        if self.grad_ready is not None:
+            self.grad_ready(net, [p + k for p in prefixes for k in ("weight", "bias")])
+
+    def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False):
         """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
-        gimg: accumulate dL/dimg (must be zeroed by the caller); keeps every gz."""
+        gimg: accumulate dL/dimg (must be zeroed by the caller); keeps every gz.
+        final: the last pass writing D's gradients this half-step (grad_ready calls)."""
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        ready = (lambda *p: self._ready("D", *p)) if final else (lambda *p: None)
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
         if GR is not None:
             ops.linear_wgrad(D["l1"], u, GR[dec + "weight"], GR[dec + "bias"], B=B, flags=0,
                              scale=he(d[0]))
+            ready(dec)
         ops.linear_dgrad(u, P[dec + "weight"], D["gzl1"], B=B, flags=L.LIN_MASK, scale=he(d[0]),
                          slope=SLOPE, aux=D["l1"])
         if GR is not None:
             ops.linear_wgrad(D["c"], D["gzl1"], GR[lin + "weight"], GR[lin + "bias"], B=B,
                              flags=L.LIN_IN_CHW, scale=he(16 * d[0]))
+            ready(lin)
         ops.linear_dgrad(D["gzl1"], P[lin + "weight"], D["gzc"], B=B,
                          flags=L.LIN_IN_CHW | L.LIN_MASK, scale=he(16 * d[0]), slope=SLOPE,
                          aux=D["c"])
@@ -572,6 +598,7 @@ class StepEngine:
             cv = "minibatch_normalization_block.conv.module."
             self._wgrad("D", "mb", D["m"], D["gzc"], GR[cv + "weight"], 4, d[0] + 1, d[0],
                         db=GR[cv + "bias"])
+            ready(cv)
         self._conv("D", "mb", D["gzc"], D["gm"], 4, d[0], r4(d[0] + 1), 0, dgrad=True)
         ops.mbstd_bwd(self.h_mb, D["gm"], D["gh"], B=B, HW=16, C=d[0])
         if inj_mbstd is not None:
@@ -590,6 +617,7 @@ class StepEngine:
                 if GR is not None:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
                                 db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc)
+                    ready(b)
                 self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
                            dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
@@ -599,6 +627,7 @@ class StepEngine:
                 if GR is not None:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
                                 d[i + 1], d[i], db=GR[b + "bias"])
+                    ready(b)
                 self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
             hin = D["yrgb"] if i == s - 1 else (D["hblend"] if i == s - 2 else D[f"p{i + 1}"])
@@ -606,6 +635,7 @@ class StepEngine:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
                             d[i + 1],
                             db=GR[a + "bias"])
+                ready(a)
             if i == s - 1:
                 self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
                            L.CONV_MASK, aux=D["yrgb"], dgrad=True)
@@ -621,6 +651,7 @@ class StepEngine:
         if GR is not None:
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
                              dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
+            ready(fr.format(s))
         if gimg is not None:
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg)
         if s >= 1:
@@ -629,6 +660,7 @@ class StepEngine:
                 ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True, img=img,
                                  dw=GR[fr.format(s - 1) + "weight"],
                                  db=GR[fr.format(s - 1) + "bias"])
+                ready(fr.format(s - 1))
             if gimg is not None:
                 ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True,
                                  gimg=gimg)
@@ -698,6 +730,7 @@ class StepEngine:
         GD_flat = self._GD_flat
         GD_flat.zero_()
         self.loss[:3].zero_()
+        self.loss[4:5].zero_()
         if self.s:
             ops.img_fade(real, alpha_D, D["real_in"])                       # :217-221
             xr = D["real_in"]
@@ -716,6 +749,8 @@ class StepEngine:
         else:
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
+            if hp.W_drift:
+                ops.drift(D["logit"], hp.W_drift, self.loss[4:5], D["u"])   # pggan/loss.py:94-100
             self.d_backward(PD, GD, D["u"], alpha_D, img=xr)
         if before_fake is not None:
             before_fake()
@@ -725,7 +760,7 @@ class StepEngine:
             img_fake = img_fake.clone()
         self.d_forward(PD, img_fake, alpha_D)                                   # :228
         ops.bce(D["logit"], False, 1.0, self.loss[1:2], D["u"], None)
-        self.d_backward(PD, GD, D["u"], alpha_D, img=img_fake)
+        self.d_backward(PD, GD, D["u"], alpha_D, img=img_fake, final=hp.gp_mode == "r1")
         if hp.gp_mode != "r1":
             self._wgan_gp(PD, GD, xr, img_fake, gp_eps, alpha_D)
         return xr, img_fake
@@ -741,7 +776,7 @@ class StepEngine:
         ops.gp_penalty(D["gimg"], self.hyper.W_gp, self.loss[2:3], D["gp_norms"], D["gbar"])
         tout, inj = self.d_tangent(PD, GD, D["gbar"], D["ones"], alpha)
         # upstream of the second backward: no BCE here, so no logit injection
-        self.d_backward(PD, GD, D["zeros"], alpha, img=D["interp"], inj_mbstd=inj)
+        self.d_backward(PD, GD, D["zeros"], alpha, img=D["interp"], inj_mbstd=inj, final=True)
 
     def g_step(self, PG, PD, GG, z, alpha_G, alpha_D, before_d=None):
         """G half of train_step (pggan/model.py:244-253).  before_d() runs after the
@@ -760,6 +795,12 @@ class StepEngine:
         return img
 
     def bind(self, fpG: FlatParams, fpD: FlatParams, hyper: Hyper):
+        """Attach parameter / optimizer buffers.  Re-binding the same objects is a no-op (the
+        packed weights stay valid); binding new ones first completes a deferred G update."""
+        if getattr(self, "fpG", None) is fpG and self.fpD is fpD and self.hyper is hyper:
+            return
+        if getattr(self, "_pending_G", None) is not None:
+            self._finish_G()
         self.fpG, self.fpD, self.hyper = fpG, fpD, hyper
         self._GD_flat, self._GG_flat = fpD.grad, fpG.grad
         self._pending_G = None     # deferred Adam_G (overlapped DP mode)

@@ -26,12 +26,14 @@ class LossInterface:
     def loss_dict(self):
         if self._buf is not None:
             v = self._buf.detach().float().cpu().tolist()
-            L_real, L_fake, reg, L_G = v[0], v[1], v[2], v[3]
+            L_real, L_fake, reg, L_G, drift = v[0], v[1], v[2], v[3], v[4]
             self._loss_dict.update({
                 "L_D_real": round(L_real, 4), "L_D_fake": round(L_fake, 4),
-                "L_D": round(L_real + L_fake + reg, 4), "L_G": round(L_G, 4)})
+                "L_D": round(L_real + L_fake + reg + drift, 4), "L_G": round(L_G, 4)})
             if self._mode != "r1":
+                # key names of the reference's commented-out WGAN-GP collector (pggan/loss.py:46-50)
                 self._loss_dict["L_D_gp"] = round(reg, 4)
+                self._loss_dict["L_D_eps"] = round(drift, 4)
             self._buf = None
         return self._loss_dict
 
@@ -49,4 +51,5 @@ class LossInterface:
 class WGANGPLoss(LossInterface):
     """pggan/loss.py:4-100: L_D = BCE(real,1) + BCE(fake,0) + R1 (live path);
     L_G = W_adv * BCE(fake,1).  gp_mode="wgan-gp" switches the regulariser to the
-    (dead in the reference) interpolate->D->grad-norm penalty of :54-92."""
+    (dead in the reference) interpolate->D->grad-norm penalty of :54-92 plus the drift
+    term W_drift_D * sum D(real)^2 of :94-100, both differentiated into D's gradient."""

@@ -122,7 +122,8 @@ class ProgressiveGAN:
                              beta2=float(args.beta2), W_adv=float(cfg_get(args, "W_adv", 1) or 0),
                              slope_cfg=float(cfg_get(args, "LReLU_slope", 0.2)),
                              gp_mode=cfg_get(args, "gp_mode", "r1"),
-                             W_gp=float(cfg_get(args, "W_gp", 10)))
+                             W_gp=float(cfg_get(args, "W_gp", 10)),
+                             W_drift=float(cfg_get(args, "W_drift_D", 0) or 0))
         self._engines = {}
         self._rng_step = 0
         self.global_step = 0
@@ -132,6 +133,7 @@ class ProgressiveGAN:
         self.next_scale_jump_step = 0
         self.train_dataset = None
         self.synthetic = None
+        self._exchange = None
 
     # ------------------------------------------------------------------ models
     def initialize_models(self):
@@ -158,12 +160,23 @@ class ProgressiveGAN:
                                                                   self.args.gpu_num)))
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         self._broadcast_params()
+        if self.world > 1:
+            from .dp import GradExchange
+            rd = torch.bfloat16 if cfg_get(self.args, "dp_reduce_dtype", "f32") == "bf16" \
+                else torch.float32
+            self._exchange = GradExchange(self.world, reduce_dtype=rd)
 
     def _broadcast_params(self):
         if self.world > 1:
+            self.flush()
             for net in (self.G, self.D):
                 for p in net.parameters():
                     dist.broadcast(p.data, 0)
+            self._params_changed()
+
+    def _params_changed(self):
+        for eng in self._engines.values():
+            eng.params_changed()
 
     def _flat(self, net, which):
         shapes = [(n, tuple(p.shape)) for n, p in net.named_parameters()]
@@ -185,21 +198,31 @@ class ProgressiveGAN:
 
     # ------------------------------------------------------------------ data
     def set_dataset(self):
-        """pggan/model.py:118-126; falls back to a resident synthetic batch (the benchmark
-        setting) when no dataset root exists."""
-        roots = [r for r in (cfg_get(self.args, "dataset_root_list", None) or []) if os.path.isdir(r)]
-        ds = ImageFolderDataset(roots, self.scale_index, seed=self.rank)
-        if len(ds) == 0:
+        """pggan/model.py:118-126: the images under `dataset_root_list`, 70% train split.
+
+        A configured root that does not exist, or roots holding no image, raise (the
+        reference's DataLoader fails on an empty dataset too).  The resident synthetic
+        batch (U[-1,1) reals in HBM, the benchmark setting) is used only when the config
+        asks for it with `synthetic_data: True`."""
+        R = 4 * 2 ** self.scale_index
+        if cfg_get(self.args, "synthetic_data", False):
             self.train_dataset = None
-            R = 4 * 2 ** self.scale_index
             g = torch.Generator(device=self.device).manual_seed(1000 * self.rank)
             self.synthetic = torch.rand(self.args.batch_per_gpu, 3, R, R, device=self.device,
                                         generator=g) * 2 - 1
-        else:
-            n_train = round(len(ds) * 0.7)
-            perm = np.random.default_rng(0).permutation(len(ds))
-            ds.paths = [ds.paths[i] for i in perm[:n_train]]
-            self.train_dataset = ds
+            return
+        roots = list(cfg_get(self.args, "dataset_root_list", None) or [])
+        missing = [r for r in roots if not os.path.isdir(r)]
+        if missing:
+            raise FileNotFoundError(f"dataset_root_list: no such directory: {missing}")
+        ds = ImageFolderDataset(roots, self.scale_index, seed=self.rank)
+        if len(ds) == 0:
+            raise RuntimeError(f"no images found under dataset_root_list {roots} (set "
+                               f"synthetic_data: True to train on a synthetic batch)")
+        n_train = round(len(ds) * 0.7)
+        perm = np.random.default_rng(0).permutation(len(ds))
+        ds.paths = [ds.paths[i] for i in perm[:n_train]]
+        self.train_dataset = ds
 
     def set_data_iterator(self):
         """lib/model.py:44-52: per-rank shard of a shuffled index order (DistributedSampler)."""
@@ -238,19 +261,35 @@ class ProgressiveGAN:
         key = (self.scale_index, B)
         if key not in self._engines:
             from . import _lib
+            self.flush()
             self._engines = {}   # one stage at a time: free the previous stage's buffers
             factory = type(self).ops_factory or _lib.HipOps
             eng = E.StepEngine(factory(self.dtype), self.args.depths, self.scale_index, B,
                                self.device, self.args.latent_dim)
             self._engines[key] = eng
         eng = self._engines[key]
-        eng.bind(self.fpG, self.fpD, self.hyper)
+        eng.bind(self.fpG, self.fpD, self.hyper)      # no-op unless the buffers changed
+        if self._exchange is not None:
+            eng.grad_ready = self._exchange.ready
+            if self._exchange._fp.get("G") is not self.fpG or \
+                    self._exchange._fp.get("D") is not self.fpD:
+                self._exchange.bind("G", self.fpG)
+                self._exchange.bind("D", self.fpD)
         return eng
 
     def _grad_hook(self, net, g):
-        if self.world > 1:
-            dist.all_reduce(g)
-            g.mul_(1.0 / self.world)
+        """Before each Adam step: the asynchronous bucketed RCCL all-reduce (mean) of the
+        net's live gradient (pggan_amd.dp); the engine waits on it right before Adam and
+        overlaps it with the work that does not depend on it."""
+        if self._exchange is None:
+            return None
+        return self._exchange.hook(net, g)
+
+    def flush(self):
+        """Complete a deferred G update (overlapped DP mode): call before reading G's
+        parameters outside train_step (save_checkpoint does)."""
+        for eng in self._engines.values():
+            eng.flush()
 
     def train_step(self):
         """pggan/model.py:206-255; returns [img_real, img_fake]."""
@@ -275,6 +314,7 @@ class ProgressiveGAN:
     # ------------------------------------------------------------------ schedule
     def reset_solver(self):
         """pggan/model.py:131-139."""
+        self.flush()
         self.set_dataset()
         self.set_data_iterator()
         self.set_optimizers()
@@ -293,6 +333,7 @@ class ProgressiveGAN:
 
     def change_scale(self, global_step):
         """pggan/model.py:158-174: add a block to G and D, fresh solver, reset alpha."""
+        self.flush()
         self.scale_index += 1
         self.next_scale_jump_step += self.args.max_step_at_scale[self.scale_index]
         self.G.add_block(self.args.depths[self.scale_index])
@@ -341,6 +382,7 @@ class ProgressiveGAN:
     def save_checkpoint(self, global_step):
         """pggan/model.py:50-67 + lib/checkpoint.py:22-34 (same paths and keys)."""
         from . import checkpoint
+        self.flush()
         base = self._ckpt_dict(global_step)
         checkpoint.save_checkpoint(self.G, self.opt_G, "G", dict(base))
         checkpoint.save_checkpoint(self.D, self.opt_D, "D", dict(base))
@@ -375,6 +417,7 @@ class ProgressiveGAN:
         self.D.load_state_dict(Dd["model"], strict=False)
         self.opt_G.load_state_dict(Gd["optimizer"])
         self.opt_D.load_state_dict(Dd["optimizer"])
+        self._params_changed()
 
     def save_image(self, images, step):
         """lib/utils.py:86-103: grid of up to 8 images per row, rows = tensors, [-1,1] ->

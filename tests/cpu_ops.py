@@ -347,6 +347,11 @@ class CpuOps:
         if h is not None:
             h.copy_(w * s * (1 - s) / B)
 
+    def drift(self, logits, w, loss, u):
+        lv = logits.reshape(-1)
+        loss += w * (lv * lv).sum()
+        u += 2 * w * lv
+
     def r1_penalty(self, g, B, r1, gbar):
         r1 += 0.5 * (g * g).sum() / B
         gbar.copy_(g / B)

@@ -191,6 +191,77 @@ def _store(out, key, t, full):
         out[key + "#norm"] = np.array([np.linalg.norm(flat.astype(np.float64))])
 
 
+# WGAN-GP optional mode (dead code in the reference): fixtures from the reference's own
+# get_gradient_penalty / get_drift_loss (pggan/loss.py:54-100), SURVEY §8(c) recipe incl.
+# the Tensor.get_device patch (pggan/loss.py:73 calls .get_device(), -1 on CPU)
+GP_CONFIGS = [  # (name, depths, s, B, alpha)
+    ("gp_tiny_s2_b8_a03", "tiny", 2, 8, 0.3),
+    ("gp_tiny_s1_b4_a05", "tiny", 1, 4, 0.5),
+]
+
+
+def run_gp(R, name, depths, s, B, alpha):
+    from gen_inputs import TINY_DEPTHS
+    depths = list(TINY_DEPTHS if depths == "tiny" else depths)
+    torch.manual_seed(0)
+    args = R["Config"].from_yaml(os.path.join(REF, "configs.yaml"))
+    args.beta1 = float(args.beta1)
+    args.isMaster = False
+    args.depths = depths
+    G = R["Generator"](args.latent_dim, depths[0], args.init_bias_to_zero, args.LReLU_slope,
+                       args.apply_pixel_norm, args.generator_last_activation, args.output_dim,
+                       args.equalized_lr)
+    D = R["Discriminator"](depths[0], args.init_bias_to_zero, args.LReLU_slope,
+                           args.decision_layer_size, args.apply_minibatch_norm, args.input_dim,
+                           args.equalized_lr)
+    for i in range(1, s + 1):
+        G.add_block(depths[i])
+        D.add_block(depths[i])
+    gsh, dsh = g_param_shapes(depths, s), d_param_shapes(depths, s)
+    PG = make_params(gsh, seed=1000 + 10 * s + B)
+    PD = make_params(dsh, seed=2000 + 10 * s + B)
+    G.load_state_dict({k: torch.from_numpy(v) for k, v in PG.items()})
+    D.load_state_dict({k: torch.from_numpy(v) for k, v in PD.items()})
+    G.alpha = D.alpha = alpha
+    lc = R["WGANGPLoss"](args)
+    st = make_inputs(B, 4 * 2 ** s, seed=3000 + 10 * s + B)[0]
+    real = torch.from_numpy(st["real"])
+    if s:   # the real-image fade of train_step (pggan/model.py:217-221)
+        low = torch.nn.functional.interpolate(torch.nn.functional.avg_pool2d(real, (2, 2)),
+                                              scale_factor=2, mode="nearest")
+        real = (1 - alpha) * low + alpha * real
+    img_real = real.detach().clone().requires_grad_()
+    pred_real = D(img_real)
+    with torch.no_grad():
+        img_fake = G(torch.from_numpy(st["z1"]))
+    D_dict = {"img_real": img_real, "img_fake": img_fake.detach(), "pred_real": pred_real}
+    eps = torch.from_numpy(st["gp_eps"])
+    real_rand, real_gd = torch.rand, torch.Tensor.get_device
+    torch.rand = lambda *a, **k: eps.clone()
+    torch.Tensor.get_device = lambda self: "cpu"
+    try:
+        D.zero_grad()
+        gp = lc.get_gradient_penalty(D_dict, D, backward=True)
+        grads = {k: (None if p.grad is None else p.grad.detach().clone())
+                 for k, p in D.named_parameters()}
+        drift = lc.get_drift_loss(D_dict)
+    finally:
+        torch.rand, torch.Tensor.get_device = real_rand, real_gd
+    out = {"gp": np.array([gp], np.float64), "drift": np.array([drift], np.float64),
+           "W_gp": np.array([float(args.W_gp)]), "W_drift_D": np.array([float(args.W_drift_D)]),
+           "img_real": img_real.detach().numpy().astype(np.float32),
+           "img_fake": img_fake.numpy().astype(np.float32),
+           "pred_real": pred_real.detach().numpy().astype(np.float32)}
+    for k, g in grads.items():
+        if g is None:
+            out[f"grad_D/{k}#none"] = np.zeros(0, np.float32)
+        else:
+            out[f"grad_D/{k}"] = g.numpy().astype(np.float32)
+    meta = dict(name=name, depths=depths, s=s, B=B, alpha=alpha)
+    out["meta"] = np.frombuffer(repr(meta).encode(), dtype=np.uint8)
+    return out
+
+
 SCHEDULE_ARGS = dict(max_step_at_scale=[5, 7, 9, 9], alpha_jump_start=[-1, 2, 3, 1],
                      alpha_jump_interval=[0, 1, 2, 1], alpha_jump_Ntimes=[0, 3, 2, 4],
                      depths=[8, 8, 8, 8])
@@ -234,6 +305,14 @@ def main(names):
         np.savez_compressed(os.path.join(HERE, "schedule.npz"), rows=run_schedule(R),
                             meta=np.frombuffer(repr(SCHEDULE_ARGS).encode(), dtype=np.uint8))
         print("schedule: written")
+    for (name, depths, s, B, alpha) in GP_CONFIGS:
+        if names and name not in names:
+            continue
+        out = run_gp(R, name, depths, s, B, alpha)
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **out)
+        print(f"{name}: GP {float(out['gp'][0]):.6e} drift {float(out['drift'][0]):.6e}, "
+              f"{os.path.getsize(path) / 1e6:.2f} MB")
     for (name, depths, s, B, alpha, n_steps, full) in GOLDEN_CONFIGS:
         if names and name not in names:
             continue

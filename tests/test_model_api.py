@@ -38,7 +38,8 @@ def _cpu_ops(monkeypatch):
 def make_args(tmp_path, **over):
     a = Config.from_yaml(os.path.join(ROOT, "pggan_amd", "default_config.yaml"))
     a.update(depths=list(TINY_DEPTHS), batch_per_gpu=4, compute_dtype="f32",
-             save_root=str(tmp_path), run_id="t", isMaster=False, dataset_root_list=[])
+             save_root=str(tmp_path), run_id="t", isMaster=False, dataset_root_list=[],
+             synthetic_data=True)
     a.update(over)
     return a
 
@@ -98,32 +99,38 @@ def test_schedule_matches_reference(tmp_path):
 
 def test_train_step_is_reference_step(tmp_path):
     """One ProgressiveGAN.train_step at stage 1, alpha 0.5 == oracle train_step on the
-    same parameters, reals and latents (latents read back from the model)."""
+    same parameters, reals and latents (latents read back from the model), replayed in
+    float64 with the engine's leaky-ReLU region choices (tests/kink_parity.py)."""
+    import kink_parity as K
     args = make_args(tmp_path)
     m = fresh_model(args)
     m.change_scale(0)
     m.G.alpha = m.D.alpha = 0.5
-    PG0 = {k: v.detach().clone() for k, v in m.G.state_dict().items()}
-    PD0 = {k: v.detach().clone() for k, v in m.D.state_dict().items()}
+    PG0 = {k: v.detach().double().clone() for k, v in m.G.state_dict().items()}
+    PD0 = {k: v.detach().double().clone() for k, v in m.D.state_dict().items()}
+    rec = K.Recorder()
+    m._engine(args.batch_per_gpu).trace = rec
     img_real, img_fake = m.train_step()
-    real = m.synthetic.clone()
-    z1, z2 = m._z[0].clone(), m._z[1].clone()
+    real = m.synthetic.clone().double()
+    z1, z2 = m._z[0].clone().double(), m._z[1].clone().double()
     ref = O.train_step(PG0, PD0, O.AdamState(args.lr_G), O.AdamState(args.lr_D), real, z1, z2,
-                       1, 0.5, 0.5)
+                       1, 0.5, 0.5, kinks=rec.seq)
     L = m.loss_collector.loss_dict
     assert abs(L["L_D_real"] - round(ref.L_D_real, 4)) <= 2e-4
     assert abs(L["L_D_fake"] - round(ref.L_D_fake, 4)) <= 2e-4
     assert abs(L["L_G"] - round(ref.L_G, 4)) <= 2e-4
     assert rel_l2(img_real.numpy(), ref.img_real.numpy()) < 1e-6
-    assert rel_l2(img_fake.numpy(), ref.img_fake_G.numpy()) < 1e-4
-    for k, g in ref.grads_D.items():
-        if g is None:
-            continue
-        got = dict(m.D.named_parameters())[k].grad
-        assert rel_l2(got.numpy(), g.numpy()) < 1e-3, k
+    assert rel_l2(img_fake.numpy(), ref.img_fake_G.numpy()) < 1e-5
+    for net, grads in ((m.D, ref.grads_D), (m.G, ref.grads_G)):
+        for k, g in grads.items():
+            if g is None:
+                continue
+            got = dict(net.named_parameters())[k].grad
+            assert rel_l2(got.numpy(), g.numpy()) < 1e-3, k
     # parameters after both Adam steps
-    for k, p in PD0.items():
-        assert rel_l2(dict(m.D.named_parameters())[k].detach().numpy(), p.numpy()) < 1e-5, k
+    for net, P0 in ((m.D, PD0), (m.G, PG0)):
+        for k, p in P0.items():
+            assert rel_l2(dict(net.named_parameters())[k].detach().numpy(), p.numpy()) < 1e-5, k
 
 
 def test_checkpoint_round_trip(tmp_path):
