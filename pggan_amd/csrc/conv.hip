@@ -1023,9 +1023,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int o = o0 + tid;
       if (p.mode == WG_SLABS)
         p.ws[blockIdx.z * p.slab + (size_t)p.cout * p.cin * 9 + o] = s;
-      else if (p.mode == WG_DIRECT)
-        p.db[o] += s * p.scale;
-      else
+      else   // WG_DIRECT: sole writer, one add like a read-modify-write (see the dW epilogue)
         atomicAdd(p.db + o, s * p.scale);
     }
   }
@@ -1068,22 +1066,18 @@ void wgrad_bf16_kernel(WgBParams p) {
       v[k2] = sum;
       offs[k2] = (o < p.cout && c < p.cin) ? (o * p.cin + c) * 9 + tap : -1;
     }
-    if (p.mode == WG_DIRECT) {
-      // all loads first, then all stores (one DRAM round trip instead of NPT)
-      float old[NPT];
-#pragma unroll
-      for (int k2 = 0; k2 < NPT; ++k2) old[k2] = offs[k2] >= 0 ? p.dw[offs[k2]] : 0.f;
-#pragma unroll
-      for (int k2 = 0; k2 < NPT; ++k2)
-        if (offs[k2] >= 0) p.dw[offs[k2]] = old[k2] + v[k2] * p.scale;
-    } else if (p.mode == WG_SLABS) {
-#pragma unroll
-      for (int k2 = 0; k2 < NPT; ++k2)
-        if (offs[k2] >= 0) slab[offs[k2]] = v[k2];
-    } else {
+    if (p.mode == WG_DIRECT || p.mode == WG_ATOMIC) {
+      // one fp32 add per element into dW.  WG_DIRECT: this workgroup is the only writer in
+      // the launch, so the (no-return, fire-and-forget) atomic performs the same single
+      // add old + v*scale as a read-modify-write, without a dependent load round trip per
+      // round (the order of adds into dW across launches stays stream order)
 #pragma unroll
       for (int k2 = 0; k2 < NPT; ++k2)
         if (offs[k2] >= 0) atomicAdd(p.dw + offs[k2], v[k2] * p.scale);
+    } else {
+#pragma unroll
+      for (int k2 = 0; k2 < NPT; ++k2)
+        if (offs[k2] >= 0) slab[offs[k2]] = v[k2];
     }
   }
 }

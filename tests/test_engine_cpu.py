@@ -70,3 +70,46 @@ def test_engine_schedule_unfused_pixelnorm():
     meta, z = load(name)
     eng, fpG, fpD = build(meta, CpuOps(fused=False))
     run_and_check(meta, z, eng, fpG, fpD, tol=1e-3)
+
+
+GP_NAMES = ["gp_tiny_s2_b8_a03", "gp_tiny_s1_b4_a05"]
+
+
+def build_gp(meta, ops, device="cpu"):
+    """Engine in the optional WGAN-GP mode with the fixture's parameters (same seeds as
+    make_golden.run_gp) and the reference configuration's W_gp / W_drift_D."""
+    m = dict(meta, n_steps=1)
+    eng, fpG, fpD = build(m, ops, device)
+    eng.hyper = E.Hyper(gp_mode="wgan-gp", W_gp=10.0, W_drift=0.001)
+    eng.bind(fpG, fpD, eng.hyper)
+    return eng, fpG, fpD
+
+
+def run_gp_and_check(name, ops, device="cpu", tol=1e-3, bf16=False):
+    """The WGAN-GP step (BCE + penalty + drift in the D gradient, pggan/loss.py:54-100)
+    against the kink-injected oracle replay, and the penalty / drift values against the
+    reference's own functions on the same inputs (fixture)."""
+    meta, z = load(name)
+    eng, fpG, fpD = build_gp(meta, ops, device)
+    s, B, alpha = meta["s"], meta["B"], meta["alpha"]
+    st = make_inputs(B, 4 * 2 ** s, seed=3000 + 10 * s + B)[0]
+    real, z1, z2, eps = (torch.from_numpy(st[k]) for k in ("real", "z1", "z2", "gp_eps"))
+    ours, ref, kinks = K.run_step(eng, fpG, fpD, real, z1, z2, alpha, gp_eps=eps,
+                                  feed_images=bf16)
+    if bf16:
+        rep = K.compare_bf16(ours, ref, fpG, fpD, kinks, loss_rtol=2e-2, min_cos=0.99,
+                             flip_bound=K.FLIP_BOUND[torch.bfloat16], img_rtol=5e-2)
+    else:
+        rep = K.compare(ours, ref, fpG, fpD, kinks, tol=tol, flip_bound=1e-4, ptol=1e-5)
+        # the penalty and the drift against the reference's own get_gradient_penalty /
+        # get_drift_loss, evaluated on the reference's images (our images match them)
+        assert abs(ours["reg"] - z["gp"][0]) <= 2e-3 * abs(z["gp"][0]) + 1.05 * abs(ref["reg"] - z["gp"][0])
+        assert abs(ours["drift"] - z["drift"][0]) <= 2e-3 * abs(z["drift"][0]) + 1e-9
+    assert ours["drift"] > 0.0 and ours["reg"] > 0.0
+    return rep
+
+
+@pytest.mark.parametrize("name", GP_NAMES)
+def test_engine_wgan_gp_step(name):
+    torch.set_num_threads(4)
+    run_gp_and_check(name, CpuOps())

@@ -65,3 +65,16 @@ def test_hip_step_bf16_vs_oracle(name):
     rep = K.compare_bf16(ours, ref, fpG, fpD, kinks, loss_rtol=2e-2, min_cos=0.99,
                          flip_bound=K.FLIP_BOUND[torch.bfloat16], img_rtol=5e-2)
     print(K.summarize(rep))
+
+
+@pytest.mark.parametrize("name", ["gp_tiny_s2_b8_a03", "gp_tiny_s1_b4_a05"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_hip_wgan_gp_step(name, dtype):
+    """The optional WGAN-GP mode on the HIP kernels (interpolate -> D -> per-sample gradient
+    norm -> double-backward, plus the drift term): kink-resolved against the oracle, and the
+    penalty / drift against the reference's own get_gradient_penalty / get_drift_loss."""
+    from pggan_amd import _lib
+    from test_engine_cpu import run_gp_and_check
+    rep = run_gp_and_check(name, _lib.HipOps(dtype), device="cuda",
+                           bf16=dtype == torch.bfloat16)
+    print(K.summarize(rep))

@@ -61,3 +61,36 @@ def test_oracle_matches_reference(name):
                 check_tensor(z, f"{pre}param_{net}/{k}", p.numpy(), 1e-6)
 
     run_oracle(meta, cb)
+
+
+GP_NAMES = ["gp_tiny_s2_b8_a03", "gp_tiny_s1_b4_a05"]
+
+
+@pytest.mark.parametrize("name", GP_NAMES)
+def test_oracle_wgan_gp_matches_reference(name):
+    """The optional WGAN-GP mode: the oracle's penalty and drift against the reference's
+    own get_gradient_penalty / get_drift_loss (pggan/loss.py:54-100; fixture made by
+    tests/golden/make_golden.py with the SURVEY §8(c) get_device patch): the penalty
+    value, its gradient w.r.t. every D parameter (backward=True), and the drift value."""
+    torch.set_num_threads(4)
+    meta, z = load(name)
+    depths, s, B, alpha = meta["depths"], meta["s"], meta["B"], meta["alpha"]
+    PD = {k: torch.from_numpy(v).requires_grad_() for k, v in
+          make_params(O.d_param_shapes(depths, s), seed=2000 + 10 * s + B).items()}
+    st = make_inputs(B, 4 * 2 ** s, seed=3000 + 10 * s + B)[0]
+    xr, xf = torch.from_numpy(z["img_real"]), torch.from_numpy(z["img_fake"])
+    pred_real = O.discriminator_forward(PD, xr, s, alpha)
+    check_tensor(z, "pred_real", pred_real.detach().numpy(), 2e-5)
+    gp = O.wgan_gp(lambda t: O.discriminator_forward(PD, t, s, alpha), xr, xf,
+                   torch.from_numpy(st["gp_eps"]), float(z["W_gp"][0]))
+    assert abs(float(gp) - z["gp"][0]) <= 1e-5 * abs(z["gp"][0])
+    names = list(PD)
+    grads = torch.autograd.grad(gp, [PD[k] for k in names], allow_unused=True)
+    for k, g in zip(names, grads):
+        key = f"grad_D/{k}"
+        if g is None:
+            assert key + "#none" in z.files, k
+            continue
+        check_tensor(z, key, g.numpy(), 1e-4)
+    drift = O.drift_loss(pred_real, float(z["W_drift_D"][0]))
+    assert abs(float(drift) - z["drift"][0]) <= 1e-5 * abs(z["drift"][0]) + 1e-12
