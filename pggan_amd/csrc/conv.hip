@@ -1125,6 +1125,10 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // channels, the gz tile is staged once for both): A/B -5..-22 % at 32^2-256^2 for
   // cin > 32; below 32^2 the single-half tile is faster
   pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32) ? 2 : 1;
+  // ... unless the single-half tiles overflow one round of workgroups (the 513-channel
+  // minibatch-stddev conv at 4^2: 8 x 33 = 264 > 256 ran as two rounds, 29.6 us vs 15.8)
+  if (pl.WNC == 1 && ci > 16 && pg_cdiv(co, co <= 16 ? 16 : co <= 32 ? 32 : 64) * pg_cdiv(ci, 16) > 256)
+    pl.WNC = 2;
   if (const char* e = getenv("PG_WG_WNC")) { if (ci > 16) pl.WNC = atoi(e); }   // tuning runs only
   const int BO = pl.WMO * pl.MO * 16, BC = pl.WNC * pl.NC * 16;
   // A/B (tools/wgbp_ab.sh): 256-pixel tiles -6..-10 % at 32^2-128^2 for the single-half
@@ -1521,6 +1525,7 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 }
 
 #include "conv_hr.inc"
+#include "conv_lr.inc"
 
 // Which fused epilogues the kernel the dispatcher picks supports.
 template <typename T>
@@ -1562,6 +1567,7 @@ int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const f
   PG_CHECK_ARG(conv_supported<T>(d, wsb), "conv3x3_fwd: flags 0x%x not supported for cout %d at %dx%d",
                d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
+    if (conv_lr_ok(d)) return conv_lr_dispatch(d, x, wpk, bias, aux, y, y2, st);
     if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, xbits, st);
   }
   int BM, BN;

@@ -164,8 +164,11 @@ class Hyper:
 class StepEngine:
     """All device buffers and kernel schedules for one (stage, batch, dtype)."""
 
-    def __init__(self, ops, depths, s, B, device, latent_dim=512):
+    def __init__(self, ops, depths, s, B, device, latent_dim=512, forward_only=None):
+        """forward_only: "G" or "D" allocates just that net's forward activations (the
+        inference / sampling path of nets.Generator / nets.Discriminator.forward)."""
         self.ops, self.depths, self.s, self.B = ops, list(depths), s, B
+        self.forward_only = forward_only
         self.dev = device
         self.dt = ops.tdtype
         self.latent = latent_dim
@@ -197,83 +200,96 @@ class StepEngine:
     def _alloc(self):
         B, s, d, R = self.B, self.s, self.depths, self.R
         t = self._t
+        fo = self.forward_only
+        # forward_only: None (the training step), "G" / "D" (that net's forward), "Gtrain" /
+        # "Dtrain" (that net's forward + first-order backward: the autograd modules)
+        need_G, need_D = fo in (None, "G", "Gtrain"), fo in (None, "D", "Dtrain")
+        train = fo in (None, "Gtrain", "Dtrain")
         # ---- G
         self.g = g = {}
-        g["z"] = t(B, self.latent, f32=True)
-        g["zn"] = t(B, self.latent, f32=True)
-        g["f"] = t(B, 4, 4, d[0])
-        g["h0"] = t(B, 4, 4, d[0])
-        g["u0"] = t(B, 4, 4, d[0])
-        g["y0"] = t(B, 4, 4, d[0])
-        g["r0"] = t(B, 4, 4, 1, f32=True)
-        for i in range(s):
-            Ri = 8 * 2 ** i
-            for k in ("ua", "ya", "ub", "yb", "gzb", "gya", "gza"):
-                g[f"{k}{i}"] = t(B, Ri, Ri, d[i + 1])
-            # per-pixel PixelNorm factors of the fused conv epilogues (G-half backward)
-            g[f"ra{i}"] = t(B, Ri, Ri, 1, f32=True)
-            g[f"rb{i}"] = t(B, Ri, Ri, 1, f32=True)
-        g["img"] = t(B, 3, R, R, f32=True)
-        # gradient wrt level outputs: lvl 0 = y0 (4x4), lvl i+1 = yb_i
-        for j in range(s + 1):
-            Rj = 4 * 2 ** j
-            g[f"gy{j}"] = t(B, Rj, Rj, d[j])
-        g["gz0"] = t(B, 4, 4, d[0])
-        g["gh0"] = t(B, 4, 4, d[0])
-        g["gzf"] = t(B, 4, 4, d[0])
+        if need_G:
+            g["z"] = t(B, self.latent, f32=True)
+            g["zn"] = t(B, self.latent, f32=True)
+            g["f"] = t(B, 4, 4, d[0])
+            g["h0"] = t(B, 4, 4, d[0])
+            g["u0"] = t(B, 4, 4, d[0])
+            g["y0"] = t(B, 4, 4, d[0])
+            g["r0"] = t(B, 4, 4, 1, f32=True)
+            for i in range(s):
+                Ri = 8 * 2 ** i
+                for k in ("ua", "ya", "ub", "yb") + (("gzb", "gya", "gza") if train else ()):
+                    g[f"{k}{i}"] = t(B, Ri, Ri, d[i + 1])
+                # per-pixel PixelNorm factors of the fused conv epilogues (G-half backward)
+                g[f"ra{i}"] = t(B, Ri, Ri, 1, f32=True)
+                g[f"rb{i}"] = t(B, Ri, Ri, 1, f32=True)
+            g["img"] = t(B, 3, R, R, f32=True)
+        if need_G and train:
+            # gradient wrt level outputs: lvl 0 = y0 (4x4), lvl i+1 = yb_i
+            for j in range(s + 1):
+                Rj = 4 * 2 ** j
+                g[f"gy{j}"] = t(B, Rj, Rj, d[j])
+            g["gz0"] = t(B, 4, 4, d[0])
+            g["gh0"] = t(B, 4, 4, d[0])
+            g["gzf"] = t(B, 4, 4, d[0])
         # ---- D
         self.dd = D = {}
-        D["yrgb"] = t(B, R, R, d[s])
-        D["gzrgb"] = t(B, R, R, d[s])
-        D["trgb"] = t(B, R, R, d[s])
-        if s >= 1:
-            D["yd"] = t(B, R // 2, R // 2, d[s - 1])
-            D["gzd"] = t(B, R // 2, R // 2, d[s - 1])
-            D["td"] = t(B, R // 2, R // 2, d[s - 1])
-            D["hblend"] = t(B, R // 2, R // 2, d[s - 1])
-            D["tblend"] = t(B, R // 2, R // 2, d[s - 1])
-        for i in range(s):
-            Ri = 8 * 2 ** i
-            # lrelu sign bits of the pre-pool conv-b output (used instead of bf{i} where the
-            # kernels support it, see _dbits)
-            D[f"mb{i}"] = torch.zeros(B, Ri, Ri, (d[i] + 7) // 8, dtype=torch.uint8, device=self.dev)
-            D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
-            D[f"bf{i}"] = t(B, Ri, Ri, d[i])
-            D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
-            D[f"gzb{i}"] = t(B, Ri, Ri, d[i])
-            D[f"gza{i}"] = t(B, Ri, Ri, d[i + 1])
-            D[f"ghin{i}"] = t(B, Ri, Ri, d[i + 1])
-            D[f"ta{i}"] = t(B, Ri, Ri, d[i + 1])
-            D[f"tbf{i}"] = t(B, Ri, Ri, d[i])
-            D[f"tp{i}"] = t(B, Ri // 2, Ri // 2, d[i])
-        D["m"] = t(B, 4, 4, self.mcs)
-        D["c"] = t(B, 4, 4, d[0])
-        D["l1"] = t(B, d[0])
-        D["logit"] = t(B, 1, f32=True)
-        D["gzl1"] = t(B, d[0])
-        D["gzc"] = t(B, 4, 4, d[0])
-        D["gm"] = t(B, 4, 4, self.mcs)
-        D["gh"] = t(B, 4, 4, d[0])
-        D["tm"] = t(B, 4, 4, self.mcs)
-        D["inj"] = t(B, 4, 4, d[0])
-        D["tc"] = t(B, 4, 4, d[0])
-        D["tl1"] = t(B, d[0])
-        D["tout"] = t(B, 1, f32=True)
-        D["u"] = t(B, f32=True)
-        D["u2"] = t(B, f32=True)
-        D["hl"] = t(B, f32=True)
-        D["gimg"] = t(B, 3, R, R, f32=True)
-        D["gbar"] = t(B, 3, R, R, f32=True)
-        D["real"] = t(B, 3, R, R, f32=True)
-        if s >= 1:
-            D["real_in"] = t(B, 3, R, R, f32=True)
-        # WGAN-GP optional mode
-        D["interp"] = t(B, 3, R, R, f32=True)
-        D["gp_eps"] = t(B, 1, f32=True)
-        D["gp_norms"] = t(B, f32=True)
-        D["ones"] = torch.full((B,), 1.0, dtype=torch.float32, device=self.dev)
-        D["zeros"] = torch.zeros((B,), dtype=torch.float32, device=self.dev)
-        # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G
+        if need_D:
+            D["yrgb"] = t(B, R, R, d[s])
+            if s >= 1:
+                D["yd"] = t(B, R // 2, R // 2, d[s - 1])
+                D["hblend"] = t(B, R // 2, R // 2, d[s - 1])
+            for i in range(s):
+                Ri = 8 * 2 ** i
+                # lrelu sign bits of the pre-pool conv-b output (used instead of bf{i} where
+                # the kernels support it, see _dbits)
+                D[f"mb{i}"] = torch.zeros(B, Ri, Ri, (d[i] + 7) // 8, dtype=torch.uint8,
+                                          device=self.dev)
+                D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
+                D[f"bf{i}"] = t(B, Ri, Ri, d[i])
+                D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
+            D["m"] = t(B, 4, 4, self.mcs)
+            D["c"] = t(B, 4, 4, d[0])
+            D["l1"] = t(B, d[0])
+            D["logit"] = t(B, 1, f32=True)
+        if need_D and train:
+            D["gzrgb"] = t(B, R, R, d[s])
+            D["trgb"] = t(B, R, R, d[s])
+            if s >= 1:
+                D["gzd"] = t(B, R // 2, R // 2, d[s - 1])
+                D["td"] = t(B, R // 2, R // 2, d[s - 1])
+                D["tblend"] = t(B, R // 2, R // 2, d[s - 1])
+            for i in range(s):
+                Ri = 8 * 2 ** i
+                D[f"gzb{i}"] = t(B, Ri, Ri, d[i])
+                D[f"gza{i}"] = t(B, Ri, Ri, d[i + 1])
+                D[f"ghin{i}"] = t(B, Ri, Ri, d[i + 1])
+                D[f"ta{i}"] = t(B, Ri, Ri, d[i + 1])
+                D[f"tbf{i}"] = t(B, Ri, Ri, d[i])
+                D[f"tp{i}"] = t(B, Ri // 2, Ri // 2, d[i])
+            D["gzl1"] = t(B, d[0])
+            D["gzc"] = t(B, 4, 4, d[0])
+            D["gm"] = t(B, 4, 4, self.mcs)
+            D["gh"] = t(B, 4, 4, d[0])
+            D["tm"] = t(B, 4, 4, self.mcs)
+            D["inj"] = t(B, 4, 4, d[0])
+            D["tc"] = t(B, 4, 4, d[0])
+            D["tl1"] = t(B, d[0])
+            D["tout"] = t(B, 1, f32=True)
+            D["u"] = t(B, f32=True)
+            D["u2"] = t(B, f32=True)
+            D["hl"] = t(B, f32=True)
+            D["gimg"] = t(B, 3, R, R, f32=True)
+            D["gbar"] = t(B, 3, R, R, f32=True)
+            D["real"] = t(B, 3, R, R, f32=True)
+            if s >= 1:
+                D["real_in"] = t(B, 3, R, R, f32=True)
+            # WGAN-GP optional mode
+            D["interp"] = t(B, 3, R, R, f32=True)
+            D["gp_eps"] = t(B, 1, f32=True)
+            D["gp_norms"] = t(B, f32=True)
+            D["ones"] = torch.full((B,), 1.0, dtype=torch.float32, device=self.dev)
+            D["zeros"] = torch.zeros((B,), dtype=torch.float32, device=self.dev)
+        # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
         self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
 
     # ------------------------------------------------------------------ weights
@@ -296,7 +312,7 @@ class StepEngine:
     def alloc_packs(self):
         ops = self.ops
         self.packs = {}
-        for net in ("G", "D"):
+        for net in (("G", "D") if self.forward_only is None else (self.forward_only[0],)):
             for key, _, cout, cin in self._conv_list(net):
                 nf = ops.packed_elems(L.PACK_FWD, cout, cin)
                 nd = ops.packed_elems(L.PACK_DGRAD, cout, cin)

@@ -4,9 +4,10 @@ attribute `alpha`, `forward(z)` / `forward(x, get_feature=False)`, and the exact
 `state_dict` keys of the reference (``blocks.{i}.block.{0,3}.module.weight`` ...),
 so reference checkpoints load unchanged.
 
-Compute goes through the HIP kernels (pggan_amd.engine).  forward() is the
-inference / sampling path (no autograd graph); training uses the hand-scheduled
-step in ProgressiveGAN.train_step.  Non-default architecture switches that the
+Compute goes through the HIP kernels (pggan_amd.engine).  forward() is differentiable
+once (first-order backward on the HIP kernels, torch.autograd.Function) when grad is
+enabled, and a forward-only sampling path otherwise; the training step, with its R1
+double backward, is the hand-scheduled ProgressiveGAN.train_step.  Non-default architecture switches that the
 reference exposes but never uses (equalized_lr=False, apply_pixel_norm=False,
 last_activation, LReLU_slope on blocks) raise NotImplementedError.
 """
@@ -19,13 +20,24 @@ from . import engine as E
 
 
 class _Param(nn.Module):
-    """Stands in for ConstrainedLayer.module (lib/layers.py:48): holds weight/bias."""
+    """Stands in for ConstrainedLayer.module (lib/layers.py:48): holds weight/bias.
+
+    Init as the reference: W ~ N(0,1) (lib/layers.py:54); b = 0 when init_bias_to_zero
+    (:51-52), else the wrapped nn.Conv2d / nn.Linear default it keeps,
+    U(-1/sqrt(fan_in), 1/sqrt(fan_in)) with fan_in = prod(weight.shape[1:])."""
 
     def __init__(self, wshape, bshape, init_bias_to_zero=True):
         super().__init__()
         self.weight = nn.Parameter(torch.randn(*wshape))            # lib/layers.py:54
-        b = torch.zeros(*bshape) if init_bias_to_zero else torch.randn(*bshape) * 0.0
-        self.bias = nn.Parameter(b)                                  # lib/layers.py:51-52
+        if init_bias_to_zero:
+            b = torch.zeros(*bshape)                                 # lib/layers.py:51-52
+        else:
+            fan_in = 1
+            for d in wshape[1:]:
+                fan_in *= int(d)
+            bound = 1.0 / fan_in ** 0.5
+            b = torch.empty(*bshape).uniform_(-bound, bound)
+        self.bias = nn.Parameter(b)
 
 
 class _Eq(nn.Module):
@@ -83,15 +95,104 @@ _ENGINES = {}
 OPS_FACTORY = None   # tests may substitute a CPU double; default: the HIP library
 
 
-def _engine(ops_dtype, depths, s, B, device):
+def _engine(net, ops_dtype, depths, s, B, device):
+    """The engine of one net: "G" / "D" hold the forward activations only (sampling),
+    "Gtrain" / "Dtrain" also that net's backward buffers (the autograd path); at most one
+    cached per kind (a new shape, dtype or stage replaces it), so sampling at 1024^2 does
+    not keep a training-sized buffer set alive."""
     from . import _lib
     key = (ops_dtype, tuple(depths), s, B, str(device))
-    if key not in _ENGINES:
+    cur = _ENGINES.get(net)
+    if cur is None or cur[0] != key:
+        _ENGINES.pop(net, None)
         factory = OPS_FACTORY or _lib.HipOps
-        eng = E.StepEngine(factory(ops_dtype), depths, s, B, device)
+        eng = E.StepEngine(factory(ops_dtype), depths, s, B, device, forward_only=net)
         eng.hyper = E.Hyper()
-        _ENGINES[key] = eng
-    return _ENGINES[key]
+        eng.fwd_version = 0
+        _ENGINES[net] = (key, eng)
+    return _ENGINES[net][1]
+
+
+def _wants_grad(x, module):
+    return torch.is_grad_enabled() and (x.requires_grad or
+                                        any(p.requires_grad for p in module.parameters()))
+
+
+def _no_double_backward():
+    if torch.is_grad_enabled():
+        raise NotImplementedError(
+            "pggan_amd modules are differentiable once (first-order backward on the HIP "
+            "kernels); the R1 double backward runs hand-scheduled in ProgressiveGAN.train_step")
+
+
+def _check_version(ctx):
+    if ctx.eng.fwd_version != ctx.version:
+        raise RuntimeError("pggan_amd: a later forward of this module overwrote the activations "
+                           "this backward needs; call backward before the next forward")
+
+
+class _GFn(torch.autograd.Function):
+    """Generator forward / first-order backward on the HIP kernels (pggan/nets.py:121-161;
+    the gradient w.r.t. every parameter; the latent receives none, as in the reference
+    where z never requires grad)."""
+
+    @staticmethod
+    def forward(ctx, module, z, *params):
+        names = [n for n, _ in module.named_parameters()]
+        P = dict(zip(names, params))
+        eng = _engine("Gtrain", module.compute_dtype, module.block_depths, module.scale_index,
+                      z.shape[0], z.device)
+        eng.hyper.slope_cfg = module.LReLU_slope
+        eng.fwd_version += 1
+        ctx.eng, ctx.version, ctx.names, ctx.alpha = eng, eng.fwd_version, names, float(module.alpha)
+        ctx.P = P
+        eng.pack("G", P)
+        return eng.g_forward(P, z.reshape(z.shape[0], -1).float(), ctx.alpha).clone()
+
+    @staticmethod
+    def backward(ctx, gimg):
+        _no_double_backward()
+        _check_version(ctx)
+        GR = {n: torch.zeros_like(p) for n, p in ctx.P.items()}
+        ctx.eng.g_backward(ctx.P, GR, gimg.float().contiguous(), ctx.alpha)
+        dead = E.dead_params("G", ctx.eng.s)     # unused at this stage: grad None, as in torch
+        return (None, None) + tuple(None if n in dead else GR[n] for n in ctx.names)
+
+
+class _DFn(torch.autograd.Function):
+    """Discriminator forward / first-order backward (pggan/nets.py:248-276): gradients
+    w.r.t. every parameter and the input image, from the logit's gradient."""
+
+    @staticmethod
+    def forward(ctx, module, x, *params):
+        names = [n for n, _ in module.named_parameters()]
+        P = dict(zip(names, params))
+        eng = _engine("Dtrain", module.compute_dtype, module.depths, module.scale_index,
+                      x.shape[0], x.device)
+        eng.fwd_version += 1
+        ctx.eng, ctx.version, ctx.names, ctx.alpha = eng, eng.fwd_version, names, float(module.alpha)
+        ctx.P = P
+        ctx.set_materialize_grads(False)
+        eng.pack("D", P)
+        ctx.x = x.float().contiguous()
+        out = eng.d_forward(P, ctx.x, ctx.alpha).clone()
+        return out, eng.dd["l1"].float().clone()
+
+    @staticmethod
+    def backward(ctx, gout, gfeat):
+        _no_double_backward()
+        _check_version(ctx)
+        if gfeat is not None and bool(gfeat.ne(0).any()):
+            raise NotImplementedError("pggan_amd: gradient through the D feature output")
+        GR = {n: torch.zeros_like(p) for n, p in ctx.P.items()}
+        eng = ctx.eng
+        gx = torch.zeros_like(ctx.x)
+        u = torch.zeros(ctx.x.shape[0], dtype=torch.float32, device=ctx.x.device)
+        if gout is not None:
+            u.copy_(gout.reshape(-1))
+        eng.d_backward(ctx.P, GR, u, ctx.alpha, img=ctx.x, gimg=gx)
+        dead = E.dead_params("D", eng.s)
+        return (None, gx) + tuple(None if n in dead else GR[n] for n in ctx.names)
 
 
 class Generator(nn.Module):
@@ -122,6 +223,8 @@ class Generator(nn.Module):
 
     def add_block(self, new_depth):
         """pggan/nets.py:102-119."""
+        _ENGINES.pop("G", None)
+        _ENGINES.pop("Gtrain", None)
         prev = self.block_depths[-1]
         self.block_depths.append(new_depth)
         dev = self.latent_format_layer.module.weight.device
@@ -133,10 +236,13 @@ class Generator(nn.Module):
         return len(self.blocks)
 
     def forward(self, x):
-        """pggan/nets.py:121-161 on the HIP kernels (no autograd graph)."""
+        """pggan/nets.py:121-161 on the HIP kernels.  Differentiable once when grad is
+        enabled and a parameter requires it (_GFn); a forward-only engine otherwise."""
+        if _wants_grad(x, self):
+            return _GFn.apply(self, x, *self.parameters())
         s = self.scale_index
         B = x.shape[0]
-        eng = _engine(self.compute_dtype, self.block_depths, s, B, x.device)
+        eng = _engine("G", self.compute_dtype, self.block_depths, s, B, x.device)
         eng.hyper.slope_cfg = self.LReLU_slope
         P = dict(self.named_parameters())
         with torch.no_grad():
@@ -171,6 +277,8 @@ class Discriminator(nn.Module):
 
     def add_block(self, new_depth):
         """pggan/nets.py:227-239."""
+        _ENGINES.pop("D", None)
+        _ENGINES.pop("Dtrain", None)
         prev = self.depths[-1]
         self.depths.append(new_depth)
         dev = self.decision_layer.module.weight.device
@@ -182,10 +290,14 @@ class Discriminator(nn.Module):
         return len(self.blocks)
 
     def forward(self, x, get_feature=False):
-        """pggan/nets.py:248-276 on the HIP kernels (no autograd graph)."""
+        """pggan/nets.py:248-276 on the HIP kernels.  Differentiable once when grad is
+        enabled and the input or a parameter requires it (_DFn); forward-only otherwise."""
+        if _wants_grad(x, self):
+            out, feat = _DFn.apply(self, x, *self.parameters())
+            return (out, feat) if get_feature else out
         s = self.scale_index
         B = x.shape[0]
-        eng = _engine(self.compute_dtype, self.depths, s, B, x.device)
+        eng = _engine("D", self.compute_dtype, self.depths, s, B, x.device)
         P = dict(self.named_parameters())
         with torch.no_grad():
             eng.pack("D", P)

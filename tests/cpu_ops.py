@@ -314,9 +314,10 @@ class CpuOps:
         y.view(B, HW, -1)[..., :C + 1] = mbstd_ref(x.reshape(B, HW, -1)[..., :C])
 
     def mbstd_bwd(self, x, gy, gx, *, B, HW, C):
-        xr = x.reshape(B, HW, -1)[..., :C].detach().clone().requires_grad_()
-        out = mbstd_ref(xr)
-        g, = torch.autograd.grad(out, xr, gy.reshape(B, HW, -1)[..., :C + 1])
+        with torch.enable_grad():   # may be called inside an autograd backward (nets._DFn)
+            xr = x.reshape(B, HW, -1)[..., :C].detach().clone().requires_grad_()
+            out = mbstd_ref(xr)
+            g, = torch.autograd.grad(out, xr, gy.reshape(B, HW, -1)[..., :C + 1])
         gx.view(B, HW, -1)[..., :C] = g
 
     def mbstd_r1(self, x, a, gy, tout, inj, *, B, HW, C):

@@ -57,16 +57,23 @@ def _worker(rank, world, port, out_dir, overlap=False):
             self.w.wait()
             self.g.mul_(1.0 / world)
 
+    if overlap == "bucketed":   # the product path: pggan_amd.dp (ProgressiveGAN.set_multi_GPU)
+        from pggan_amd.dp import GradExchange
+        ex = GradExchange(world, bucket_bytes=16 << 10)
+        ex.bind("G", fpG)
+        ex.bind("D", fpD)
+        eng.grad_ready = ex.ready
+        gh = ex.hook
+    else:
+        gh = (lambda net, g: Pending(g)) if overlap else hook
     eng.train_step(torch.from_numpy(st["real"]), torch.from_numpy(st["z1"]),
-                   torch.from_numpy(st["z2"]), ALPHA, ALPHA,
-                   grad_hook=(lambda net, g: Pending(g)) if overlap else hook)
+                   torch.from_numpy(st["z2"]), ALPHA, ALPHA, grad_hook=gh)
     eng.flush()
     gD1, gG1 = fpD.grad.clone(), fpG.grad.clone()
     # a second step (the deferred G update of step 1 lands inside it in overlap mode)
     st2 = make_inputs(B, 4 * 2 ** S, seed=700 + rank)[0]
     eng.train_step(torch.from_numpy(st2["real"]), torch.from_numpy(st2["z1"]),
-                   torch.from_numpy(st2["z2"]), ALPHA, ALPHA,
-                   grad_hook=(lambda net, g: Pending(g)) if overlap else hook)
+                   torch.from_numpy(st2["z2"]), ALPHA, ALPHA, grad_hook=gh)
     eng.flush()
     np.savez(os.path.join(out_dir, f"rank{rank}_2.npz"), pD=fpD.flat.numpy(), pG=fpG.flat.numpy())
     fpD.grad.copy_(gD1)
@@ -76,10 +83,11 @@ def _worker(rank, world, port, out_dir, overlap=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("overlap", [False, True, "bucketed"])
 def test_dp_gradients_are_mean_of_shard_gradients(tmp_path, overlap):
     """overlap: the async all-reduce schedule (D exchange beside the G forward, G exchange
-    deferred into the next step) must give the same result."""
+    deferred into the next step) must give the same result; "bucketed": the product
+    path's per-layer buckets launched as the final backward pass finishes each layer."""
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), overlap), nprocs=world, join=True)
     r = [np.load(tmp_path / f"rank{i}.npz") for i in range(world)]
@@ -112,11 +120,13 @@ def test_dp_overlap_is_bitwise_identical(tmp_path):
     """Two steps with the overlapped schedule == two steps with the synchronous one."""
     world = 2
     out = {}
-    for ov in (False, True):
-        d = tmp_path / f"ov{int(ov)}"
+    for ov in (False, True, "bucketed"):
+        d = tmp_path / f"ov{ov}"
         d.mkdir()
         mp.spawn(_worker, args=(world, _free_port(), str(d), ov), nprocs=world, join=True)
         out[ov] = [np.load(d / f"rank{i}_2.npz") for i in range(world)]
     for i in range(world):
         for k in ("pD", "pG"):
             assert np.array_equal(out[False][i][k], out[True][i][k]), (i, k)
+            # bucketing changes which elements travel together, not the fp32 sums
+            assert np.array_equal(out[False][i][k], out["bucketed"][i][k]), (i, k)

@@ -58,8 +58,11 @@ def test_fused_matches_unfused_bf16(s, B, alpha, what, off):
     la, lb = a["loss"].cpu().numpy(), b["loss"].cpu().numpy()
     assert np.allclose(la[:4], lb[:4], rtol=2e-2, atol=1e-4), (what, la[:4], lb[:4])
     for k in ("img_d", "img_g"):
+        # two bf16 schedules of the 14-16-layer generator: each is ~2% from the float64
+        # oracle at these depths (profiles/r2_parity_C5_bf16.json), so they may differ by
+        # about that much from each other
         e = float((a[k] - b[k]).norm() / b[k].norm())
-        assert e <= 1e-2, (what, k, e)
+        assert e <= 3e-2, (what, k, e)
     cos = {("D", k): _cos(a["gD"][k], b["gD"][k]) for k in b["gD"] if float(b["gD"][k].norm()) > 0}
     cos.update({("G", k): _cos(a["gG"][k], b["gG"][k]) for k in b["gG"]
                 if float(b["gG"][k].norm()) > 0})

@@ -127,10 +127,14 @@ def test_train_step_is_reference_step(tmp_path):
                 continue
             got = dict(net.named_parameters())[k].grad
             assert rel_l2(got.numpy(), g.numpy()) < 1e-3, k
-    # parameters after both Adam steps
-    for net, P0 in ((m.D, PD0), (m.G, PG0)):
+    # parameters after both Adam steps: 1e-5 relative, or within 1e-3 of the Adam step
+    # size lr (zero-initialised biases are O(lr) after one step, and beta1 = 0 makes the
+    # step lr * g / (|g| + eps): last-bit differences of |g| ~ eps move it by ~1e-5 lr)
+    for net, P0, lr in ((m.D, PD0, args.lr_D), (m.G, PG0, args.lr_G)):
         for k, p in P0.items():
-            assert rel_l2(dict(net.named_parameters())[k].detach().numpy(), p.numpy()) < 1e-5, k
+            got = dict(net.named_parameters())[k].detach().numpy()
+            assert rel_l2(got, p.numpy()) < 1e-5 or \
+                float(np.abs(got - p.numpy()).max()) <= 1e-3 * lr, k
 
 
 def test_checkpoint_round_trip(tmp_path):
@@ -215,3 +219,105 @@ def test_accepts_reference_config_object(tmp_path):
     assert m.dtype == torch.float32 and m.hyper.gp_mode == "r1"
     m.train_step()
     assert np.isfinite(m.loss_collector.loss_dict["L_D"])
+
+
+def _forward_check(device="cpu", dtype=torch.float32, tol=1e-5, s=2, alpha=0.5, B=4):
+    """Generator.forward / Discriminator.forward(get_feature=True) (pggan/nets.py:121-161,
+    248-276) against the oracle on the same parameters and inputs."""
+    from gen_inputs import make_inputs, make_params
+    G = nets.Generator(512, TINY_DEPTHS[0]).to(device)
+    D = nets.Discriminator(TINY_DEPTHS[0], apply_minibatch_norm=True).to(device)
+    for i in range(1, s + 1):
+        G.add_block(TINY_DEPTHS[i])
+        D.add_block(TINY_DEPTHS[i])
+    G.alpha = D.alpha = alpha
+    G.compute_dtype = D.compute_dtype = dtype
+    PG = {k: torch.from_numpy(v) for k, v in make_params(O.g_param_shapes(TINY_DEPTHS, s), 71).items()}
+    PD = {k: torch.from_numpy(v) for k, v in make_params(O.d_param_shapes(TINY_DEPTHS, s), 72).items()}
+    G.load_state_dict(PG)
+    D.load_state_dict(PD)
+    st = make_inputs(B, 4 * 2 ** s, seed=73)[0]
+    z, x = torch.from_numpy(st["z1"]), torch.from_numpy(st["real"])
+    with torch.no_grad():   # the sampling path (forward-only engine)
+        img = G(z.to(device)).cpu()
+    ref = O.generator_forward({k: v.double() for k, v in PG.items()}, z.double(), s, alpha)
+    assert rel_l2(img.numpy(), ref.numpy()) <= tol
+    with torch.no_grad():
+        out, feat = D(x.to(device), get_feature=True)
+    ro, rf = O.discriminator_forward({k: v.double() for k, v in PD.items()}, x.double(), s, alpha,
+                                     get_feature=True)
+    assert rel_l2(out.cpu().numpy(), ro.numpy()) <= tol
+    assert rel_l2(feat.cpu().numpy(), rf.numpy()) <= tol
+    return G, D
+
+
+def test_module_forward_is_reference():
+    G, D = _forward_check()
+    # one forward-only engine per net, evicted when the net grows
+    assert set(nets._ENGINES) == {"G", "D"}
+    assert nets._ENGINES["G"][1].forward_only == "G" and "gy0" not in nets._ENGINES["G"][1].g
+    G.add_block(TINY_DEPTHS[3])
+    assert "G" not in nets._ENGINES
+
+
+def test_bias_init_follows_reference():
+    """init_bias_to_zero=False keeps nn.Conv2d / nn.Linear's default uniform bias
+    (lib/layers.py:51-52 skips the zero fill)."""
+    torch.manual_seed(0)
+    G = nets.Generator(512, 32, init_bias_to_zero=False)
+    b = G.first_block.block[0].module.bias if hasattr(G.first_block.block, "__getitem__") else \
+        getattr(G.first_block.block, "0").module.bias
+    bound = 1.0 / (32 * 9) ** 0.5
+    assert float(b.abs().max()) <= bound and float(b.abs().max()) > 0.0
+    G0 = nets.Generator(512, 32)
+    assert float(G0.latent_format_layer.module.bias.abs().max()) == 0.0
+
+
+def _autograd_check(device="cpu", dtype=torch.float32, tol=1e-4, s=2, alpha=0.5, B=4):
+    """The modules are differentiable once, like the reference's (pggan/nets.py:121-161,
+    248-276 under autograd): L = BCE(D(G(z)), 1) backpropagated through both nets gives
+    the oracle's gradients for every G and D parameter (compared kink-tolerantly at tiny
+    widths: a relative L2 bound, float64 oracle)."""
+    from gen_inputs import make_inputs, make_params
+    G = nets.Generator(512, TINY_DEPTHS[0]).to(device)
+    D = nets.Discriminator(TINY_DEPTHS[0], apply_minibatch_norm=True).to(device)
+    for i in range(1, s + 1):
+        G.add_block(TINY_DEPTHS[i])
+        D.add_block(TINY_DEPTHS[i])
+    G.alpha = D.alpha = alpha
+    G.compute_dtype = D.compute_dtype = dtype
+    PG = {k: torch.from_numpy(v) for k, v in make_params(O.g_param_shapes(TINY_DEPTHS, s), 81).items()}
+    PD = {k: torch.from_numpy(v) for k, v in make_params(O.d_param_shapes(TINY_DEPTHS, s), 82).items()}
+    G.load_state_dict(PG)
+    D.load_state_dict(PD)
+    z = torch.from_numpy(make_inputs(B, 4 * 2 ** s, seed=83)[0]["z1"])
+    img = G(z.to(device))
+    out, _ = D(img, get_feature=True)
+    assert img.requires_grad and out.requires_grad, (torch.is_grad_enabled(), img.requires_grad)
+    L = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out))
+    L.backward()
+    P64 = lambda P: {k: v.double().requires_grad_() for k, v in P.items()}
+    RG, RD = P64(PG), P64(PD)
+    ri = O.generator_forward(RG, z.double(), s, alpha)
+    Lr = O.bce_logits(O.discriminator_forward(RD, ri, s, alpha), 1)
+    Lr.backward()
+    assert abs(float(L) - float(Lr)) <= tol * abs(float(Lr)) + 1e-6
+    errs = {}
+    for net, R in ((G, RG), (D, RD)):
+        for k, p in net.named_parameters():
+            if R[k].grad is None:
+                assert p.grad is None, k
+                continue
+            errs[k] = rel_l2(p.grad.cpu().numpy(), R[k].grad.numpy())
+    worst = max(errs.values())
+    assert worst <= tol, sorted(errs.items(), key=lambda kv: -kv[1])[:4]
+    # the double backward of the R1 penalty is not available through autograd
+    x = img.detach().clone().requires_grad_()
+    o = D(x)
+    with pytest.raises(NotImplementedError):
+        torch.autograd.grad(o.sum(), x, create_graph=True)
+    return worst
+
+
+def test_modules_are_differentiable():
+    _autograd_check()

@@ -1,10 +1,16 @@
 """Summarise a rocprofv3 --pmc CSV (per-kernel mean of each counter over dispatches)."""
 import collections
 import csv
+import glob
+import os
 import sys
 
 for d in sys.argv[1:]:
-    rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
+    hits = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))
+    if not hits:
+        print(d, "no counter_collection.csv")
+        continue
+    rows = list(csv.DictReader(open(hits[0])))
     agg = collections.defaultdict(list)
     info = {}
     for r in rows:

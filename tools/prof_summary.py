@@ -33,6 +33,27 @@ def short(name):
     return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
 
 
+def gap_stats(path):
+    """Idle time of the GPU between consecutive kernels (same queue order, by start time):
+    sum of positive gaps and the number of kernels, over the whole trace."""
+    path = _resolve(path, "kernel_trace.csv")
+    ev = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    ev.sort()
+    gaps, last_end, small = 0, None, 0
+    for a, b in ev:
+        if last_end is not None and a > last_end:
+            g = a - last_end
+            if g < 1_000_000:      # ignore host-side pauses (> 1 ms) between phases
+                gaps += g
+                small += 1
+        last_end = b if last_end is None else max(last_end, b)
+    return dict(kernels=len(ev), gap_ms=gaps / 1e6, gaps_counted=small,
+                avg_gap_us=gaps / 1e3 / max(small, 1))
+
+
 def read_trace(path):
     path = _resolve(path, "kernel_trace.csv")
     fam = defaultdict(lambda: dict(ns=0, calls=0, dispatches=0))
@@ -93,7 +114,7 @@ def main():
     a = ap.parse_args()
     fam, per_kernel, total = read_trace(a.trace)
     res = {"config": a.config, "total_kernel_ms": total / 1e6, "families": {},
-           "top_kernels": []}
+           "top_kernels": [], "gaps": gap_stats(a.trace)}
     for k, v in fam.items():
         res["families"][k] = dict(total_ms=v["ns"] / 1e6, calls=v["calls"],
                                   dispatches=v["dispatches"],
