@@ -400,7 +400,12 @@ def main():
             "config": {"workload": f"{CONFIG_NAME.get((s, B), 'custom')} G+D+"
                                    f"{'R1' if args.gp_mode == 'r1' else 'WGAN-GP'} train_step "
                                    f"via ProgressiveGAN.train_step, stage {s} ({R}x{R}), "
-                                   f"batch {B}/GPU, alpha {args.alpha}, depths {depths}",
+                                   f"batch {B}/GPU, alpha {args.alpha}, depths {depths}" +
+                                   (" (alpha = 1: the fade-in's zero-weight low-resolution "
+                                    "branches elided, results bit-identical on the CPU double, "
+                                    "PG_ELIDE_BLEND=0 computes them)"
+                                    if args.alpha == 1.0 and os.environ.get("PG_ELIDE_BLEND", "1")
+                                    != "0" else ""),
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
             "host_enqueue_ms_per_step": round(host_ms, 3),

@@ -70,13 +70,16 @@ class Kinks:
     bound, so a real kernel error (a wrong sign far from 0) cannot hide behind a mask.
 
     masks: {site: bool tensor shaped like the pre-activation (NCHW / [B, N])}, True =
-    slope 1.  Every site the forward reaches must be present."""
+    slope 1.  Every site the forward reaches must be present; None marks a branch the
+    implementation elided because its weight is exactly 0 (its own sign is used)."""
 
     def __init__(self, masks):
         self.masks = masks
         self.stats = {}
 
     def act(self, x, site, slope):
+        if self.masks[site] is None:   # a branch the implementation elided (zero weight)
+            return lrelu(x, slope)
         m = self.masks[site].to(x.device)
         assert m.shape == x.shape, (site, tuple(m.shape), tuple(x.shape))
         with torch.no_grad():

@@ -185,6 +185,13 @@ class StepEngine:
         self.fuse_pnbwd = os.environ.get("PG_PNBWD", "1") != "0"
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
+        # alpha == 1: the low-resolution branches of the fade-in (toRGB / fromRGB of the
+        # previous level, the real-image fade) are multiplied by exactly 0 in the reference
+        # (pggan/nets.py:155-156,263-265, pggan/model.py:217-221) and contribute exactly 0 to
+        # every output and gradient; elide them (bit-identical).  Their
+        # parameters still get a zero gradient and the Adam step, as in the reference.
+        self.elide_zero_blend = os.environ.get("PG_ELIDE_BLEND", "1") != "0"
+        self._last_dlow = True
         # trace(net, engine) after every G / D forward, or None: parity tests read the
         # leaky-ReLU region choices of each forward from the activation buffers
         self.trace = None
@@ -486,11 +493,19 @@ class StepEngine:
     def _ylvl(self, j):
         return self.g["y0"] if j == 0 else self.g[f"yb{j - 1}"]
 
+    def _low(self, alpha):
+        """Whether the fade-in's low-resolution branch contributes (alpha < 1 at s >= 1)."""
+        return self.s >= 1 and not (self.elide_zero_blend and alpha == 1.0)
+
+    def _top_out(self, alpha):
+        """D's output of the top block after the fade-in blend."""
+        return self.dd["hblend"] if self._low(alpha) else self.dd[f"p{self.s - 1}"]
+
     def _rgb_out(self, P, alpha):
         s, d, g = self.s, self.depths, self.g
         w = P[f"toRGB_blocks.{s}.toRGB.module.weight"]
         kw = {}
-        if s >= 1:
+        if self._low(alpha):
             kw = dict(xp=self._ylvl(s - 1), wp=P[f"toRGB_blocks.{s - 1}.toRGB.module.weight"],
                       bp=P[f"toRGB_blocks.{s - 1}.toRGB.module.bias"], cp=he(d[s - 1]), Cp=d[s - 1],
                       alpha=alpha)
@@ -500,7 +515,8 @@ class StepEngine:
     def g_backward(self, P, GR, gimg, alpha):
         ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
         kw = {}
-        if s >= 1:
+        low = self._low(alpha)
+        if low:
             pre = f"toRGB_blocks.{s - 1}.toRGB.module."
             kw = dict(xp=self._ylvl(s - 1), wp=P[pre + "weight"], cp=he(d[s - 1]), Cp=d[s - 1],
                       alpha=alpha, gxp=g[f"gy{s - 1}"], dwp=GR[pre + "weight"],
@@ -532,7 +548,8 @@ class StepEngine:
                         d[i + 1], ups=True,
                         db=GR[a + "bias"])
             self._ready("G", a)
-            flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and s >= 1) else 0)
+            # level s-1 also received the toRGB fade-in branch's gradient: accumulate
+            flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and low) else 0)
             self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
                        dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
         fb = "first_block.block.0.module."
@@ -554,7 +571,9 @@ class StepEngine:
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(img, P[fr.format(s) + "weight"], P[fr.format(s) + "bias"], he(3), D["yrgb"],
                      B=B, R=R, C=d[s], down=False, slope=SLOPE)            # nets.py:255
-        if s >= 1:
+        low = self._low(alpha)
+        self._last_dlow = low
+        if low:
             ops.from_rgb(img, P[fr.format(s - 1) + "weight"], P[fr.format(s - 1) + "bias"], he(3),
                          D["yd"], B=B, R=R // 2, C=d[s - 1], down=True, slope=SLOPE)  # :251-252
         h = D["yrgb"]
@@ -568,7 +587,7 @@ class StepEngine:
             else:
                 self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
                            L.CONV_LRELU | L.CONV_POOL, y2=D[f"bf{i}"], out_scale=0.25)
-            if i == s - 1:
+            if i == s - 1 and low:
                 ops.blend(1.0 - alpha, D["yd"], alpha, D[f"p{i}"], D["hblend"])
                 h = D["hblend"]
             else:
@@ -620,10 +639,11 @@ class StepEngine:
         if inj_mbstd is not None:
             ops.blend(1.0, D["gh"], 1.0, inj_mbstd, D["gh"])
         g = D["gh"]
+        low = self._low(alpha)
         for i in range(s):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
-            if i == s - 1:
+            if i == s - 1 and low:
                 # blend backward: the low-res branch gets (1-alpha) g (nets.py:263-265)
                 ops.unpool_mask(g, D["yd"], D["gzd"], B=B, H=Ri // 2, W=Ri // 2, C=d[i],
                                 scale=1.0 - alpha, slope=SLOPE, ups=False)
@@ -646,7 +666,7 @@ class StepEngine:
                     ready(b)
                 self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
-            hin = D["yrgb"] if i == s - 1 else (D["hblend"] if i == s - 2 else D[f"p{i + 1}"])
+            hin = D["yrgb"] if i == s - 1 else (self._top_out(alpha) if i == s - 2 else D[f"p{i + 1}"])
             if GR is not None:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
                             d[i + 1],
@@ -670,7 +690,7 @@ class StepEngine:
             ready(fr.format(s))
         if gimg is not None:
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg)
-        if s >= 1:
+        if low:
             w1 = P[fr.format(s - 1) + "weight"]
             if GR is not None:
                 ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True, img=img,
@@ -690,7 +710,8 @@ class StepEngine:
                      down=False, slope=SLOPE, mask_y=D["yrgb"])
         ops.from_rgb_bwd(D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
                          down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
-        if s >= 1:
+        low = self._low(alpha)
+        if low:
             ops.from_rgb(gbar, P[fr.format(s - 1) + "weight"], None, he(3), D["td"], B=B, R=R // 2,
                          C=d[s - 1], down=True, slope=SLOPE, mask_y=D["yd"])
             ops.from_rgb_bwd(D["gzd"], P[fr.format(s - 1) + "weight"], he(3), B=B, R=R // 2,
@@ -717,7 +738,7 @@ class StepEngine:
                 self._wgrad("D", f"b{i}", D[f"ta{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
                             d[i + 1], d[i])
                 ops.avgpool2(D[f"tbf{i}"], D[f"tp{i}"], B=B, H=Ri, W=Ri, C=d[i])
-            if i == s - 1:
+            if i == s - 1 and low:
                 ops.blend(1.0 - alpha, D["td"], alpha, D[f"tp{i}"], D["tblend"])
                 t = D["tblend"]
             else:
@@ -747,11 +768,11 @@ class StepEngine:
         GD_flat.zero_()
         self.loss[:3].zero_()
         self.loss[4:5].zero_()
-        if self.s:
+        if self._low(alpha_D):
             ops.img_fade(real, alpha_D, D["real_in"])                       # :217-221
             xr = D["real_in"]
         else:
-            xr = real
+            xr = real   # s = 0, or alpha = 1: (1 - 1) * up2(avgpool2(x)) + 1 * x == x exactly
         if hp.gp_mode == "r1":
             # ---- real: F, B1, R1, T, B2
             self.d_forward(PD, xr, alpha_D)

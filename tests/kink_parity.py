@@ -52,7 +52,8 @@ def d_masks(eng):
     D, d, s = eng.dd, eng.depths, eng.s
     m = {"rgb": _nchw(D["yrgb"], d[s]) > 0}
     if s:
-        m["rgbd"] = _nchw(D["yd"], d[s - 1]) > 0
+        # None: the engine elided the low-resolution branch (alpha = 1, weight exactly 0)
+        m["rgbd"] = _nchw(D["yd"], d[s - 1]) > 0 if eng._last_dlow else None
     for i in range(s):
         m[f"a{i}"] = _nchw(D[f"a{i}"], d[i + 1]) > 0
         if eng._dbits(i):
@@ -61,7 +62,7 @@ def d_masks(eng):
             m[f"b{i}"] = _nchw(D[f"bf{i}"], d[i]) > 0
     m["mb"] = _nchw(D["c"], d[0]) > 0
     m["lin"] = D["l1"][:, :d[0]] > 0
-    return {k: v.cpu() for k, v in m.items()}
+    return {k: (None if v is None else v.cpu()) for k, v in m.items()}
 
 
 def g_masks(eng):

@@ -113,3 +113,45 @@ def run_gp_and_check(name, ops, device="cpu", tol=1e-3, bf16=False):
 def test_engine_wgan_gp_step(name):
     torch.set_num_threads(4)
     run_gp_and_check(name, CpuOps())
+
+
+def elision_bitwise(ops_factory, device, depths, s, B, dtype=torch.float32, steps=2, rtol=0.0):
+    """alpha = 1: eliding the fade-in's exactly-zero low-resolution branches (engine
+    .elide_zero_blend) must leave every image, loss, gradient and parameter bit-identical
+    to computing them (the reference computes them, pggan/nets.py:155-156,263-265).
+    rtol > 0: the HIP step's cross-workgroup fp32 atomics (R1 sum, to/fromRGB weight
+    gradients, split slab sums) are not bitwise reproducible run to run, so there the two
+    runs are held to rtol per tensor instead."""
+    out = []
+    for elide in (False, True):
+        gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
+        PG = {k: torch.from_numpy(v) for k, v in make_params(gsh, seed=61).items()}
+        PD = {k: torch.from_numpy(v) for k, v in make_params(dsh, seed=62).items()}
+        fpG = E.FlatParams(gsh, E.dead_params("G", s), device, PG)
+        fpD = E.FlatParams(dsh, E.dead_params("D", s), device, PD)
+        eng = E.StepEngine(ops_factory(), depths, s, B, device)
+        eng.elide_zero_blend = elide
+        eng.bind(fpG, fpD, E.Hyper())
+        eng.keep_fake_D = True
+        res = []
+        for t, st in enumerate(make_inputs(B, 4 * 2 ** s, seed=63, n_steps=steps)):
+            r, z1, z2 = (torch.from_numpy(st[k]).to(device) for k in ("real", "z1", "z2"))
+            ims = eng.train_step(r, z1, z2, 1.0, 1.0)
+            eng.flush()
+            res.append([x.detach().cpu().clone() for x in ims] +
+                       [eng.loss.cpu().clone(), fpD.grad.cpu().clone(), fpG.grad.cpu().clone(),
+                        fpD.flat.cpu().clone(), fpG.flat.cpu().clone()])
+        out.append(res)
+    for t, (a, b) in enumerate(zip(*out)):
+        for i, (x, y) in enumerate(zip(a, b)):
+            if rtol == 0.0:
+                assert torch.equal(x, y), (t, i, float((x - y).abs().max()))
+            else:
+                e = float((x.double() - y.double()).norm() / max(float(y.double().norm()), 1e-30))
+                assert e <= rtol, (t, i, e)
+
+
+def test_alpha_one_elision_is_bitwise():
+    torch.set_num_threads(4)
+    from gen_inputs import TINY_DEPTHS
+    elision_bitwise(CpuOps, "cpu", TINY_DEPTHS, 3, 4)

@@ -28,6 +28,18 @@ def test_module_forward_on_hip(dtype, tol):
     _forward_check(device="cuda", dtype=dtype, tol=tol)
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-3), (torch.bfloat16, 5e-2)],
+                         ids=["f32", "bf16"])
+def test_modules_differentiable_on_hip(dtype, tol):
+    """The autograd path of the modules (first-order backward on the HIP kernels) against
+    the oracle's autograd, with the forwards' region choices injected."""
+    from pggan_amd import nets
+    from test_model_api import _autograd_check
+    nets.OPS_FACTORY = None
+    nets._ENGINES.clear()
+    _autograd_check(device="cuda", dtype=dtype, tol=tol)
+
+
 def test_progressive_transitions_on_hip(tmp_path):
     from pggan_amd import nets
     from pggan_amd.model import ProgressiveGAN

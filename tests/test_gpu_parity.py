@@ -78,3 +78,18 @@ def test_hip_wgan_gp_step(name, dtype):
     rep = run_gp_and_check(name, _lib.HipOps(dtype), device="cuda",
                            bf16=dtype == torch.bfloat16)
     print(K.summarize(rep))
+
+
+@pytest.mark.parametrize("dtype,s,rtol", [(torch.float32, 3, 1e-6), (torch.bfloat16, 6, 1e-3)],
+                         ids=["f32", "bf16"])
+def test_alpha_one_elision_on_hip(dtype, s, rtol):
+    """The benchmark runs at alpha = 1 with the exactly-zero fade-in branches elided; the
+    HIP step must equal computing them up to the run-to-run reproducibility of its fp32
+    atomics (bitwise on the CPU double, test_engine_cpu.test_alpha_one_elision_is_bitwise):
+    tiny widths in fp32, paper widths at 256^2 in bf16 (the bench's fused / sign-bit tiles;
+    one fp32 last-bit difference can flip a bf16 rounding, hence 1e-3 there)."""
+    from pggan_amd import _lib
+    from gen_inputs import TINY_DEPTHS
+    from test_engine_cpu import elision_bitwise
+    depths = TINY_DEPTHS if dtype == torch.float32 else O.PAPER_DEPTHS
+    elision_bitwise(lambda: _lib.HipOps(dtype), "cuda", depths, s, 4, dtype, rtol=rtol)

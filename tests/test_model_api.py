@@ -291,15 +291,21 @@ def _autograd_check(device="cpu", dtype=torch.float32, tol=1e-4, s=2, alpha=0.5,
     G.load_state_dict(PG)
     D.load_state_dict(PD)
     z = torch.from_numpy(make_inputs(B, 4 * 2 ** s, seed=83)[0]["z1"])
+    import kink_parity as K
     img = G(z.to(device))
     out, _ = D(img, get_feature=True)
     assert img.requires_grad and out.requires_grad, (torch.is_grad_enabled(), img.requires_grad)
+    # the forwards' leaky-ReLU region choices, injected into the oracle (kink_parity)
+    kG = O.Kinks(K.g_masks(nets._ENGINES["Gtrain"][1]))
+    kD = O.Kinks(K.d_masks(nets._ENGINES["Dtrain"][1]))
     L = torch.nn.functional.binary_cross_entropy_with_logits(out, torch.ones_like(out))
     L.backward()
     P64 = lambda P: {k: v.double().requires_grad_() for k, v in P.items()}
     RG, RD = P64(PG), P64(PD)
-    ri = O.generator_forward(RG, z.double(), s, alpha)
-    Lr = O.bce_logits(O.discriminator_forward(RD, ri, s, alpha), 1)
+    ri = O.generator_forward(RG, z.double(), s, alpha, kinks=kG)
+    # D sees our image (its value), the gradient flows into the oracle's G
+    ri_ours = ri + (img.detach().cpu().double() - ri).detach()
+    Lr = O.bce_logits(O.discriminator_forward(RD, ri_ours, s, alpha, kinks=kD), 1)
     Lr.backward()
     assert abs(float(L) - float(Lr)) <= tol * abs(float(Lr)) + 1e-6
     errs = {}
