@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--alpha", type=float, default=1.0)
     p.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0: os.cpu_count()")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0: the process's CPU share (OMP_NUM_THREADS, else os.cpu_count())")
     p.add_argument("--gp-mode", choices=["r1", "wgan-gp"], default="r1")
     p.add_argument("--no-kernel-events", action="store_true")
     return p.parse_args()
@@ -215,12 +216,23 @@ def pmc_traffic(args, fam):
     return None, None
 
 
+def host_threads():
+    """CPU threads this process may use: the pool sets OMP_NUM_THREADS to the box's CPU
+    share (16 per GPU) while os.cpu_count() reports every logical CPU of the machine (256);
+    oversubscribing that share made the baseline step run for minutes."""
+    share = os.environ.get("OMP_NUM_THREADS")
+    n = os.cpu_count() or 1
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return n
+
+
 def cpu_baseline(args, steps=1):
     """The CPU oracle (fp32 restatement of the reference step, pinned to the reference's
     golden vectors) on the host cores: one train_step at the same workload, with
-    torch.set_num_threads(os.cpu_count()) (CPU-baseline plan)."""
+    torch.set_num_threads(<the process's CPU share>) (CPU-baseline plan)."""
     from oracle import pggan_oracle as O
-    threads = args.cpu_threads or os.cpu_count() or 1
+    threads = args.cpu_threads or host_threads()
     torch.set_num_threads(threads)
     s, B = args.stage, args.batch
     depths = PAPER_DEPTHS
@@ -239,7 +251,7 @@ def cpu_baseline(args, steps=1):
         O.train_step(PG, PD, optG, optD, real, z1, z2, s, args.alpha, args.alpha)
     dt = time.perf_counter() - t0
     return dict(value=B * steps / dt, unit="images/sec", cores=threads, kind="port",
-                host_cpu_count=os.cpu_count(),
+                host_cpu_count=os.cpu_count(), omp_num_threads=os.environ.get("OMP_NUM_THREADS"),
                 sample=f"{steps} oracle train_step at {R}x{R}, batch {B}, alpha {args.alpha} "
                        f"(fp32, torch CPU, torch.set_num_threads({threads})): {dt:.1f} s")
 
@@ -305,6 +317,8 @@ def main():
     def step():
         model.train_step()
 
+    log = lambda m: print(f"[bench] {m}", file=sys.stderr, flush=True)
+    log(f"stage {s} batch {B} world {world}: {args.warmup} warm-up steps")
     for _ in range(args.warmup):
         step()
     model.flush()
@@ -346,6 +360,13 @@ def main():
     if timer and os.environ.get("PG_BENCH_SHAPES"):
         with open(os.environ["PG_BENCH_SHAPES"], "w") as f:
             json.dump(timer.per_shape(1), f, indent=1)
+    if timer and os.environ.get("PG_BENCH_LAUNCHES"):
+        # the instrumented step's conv / wgrad calls in launch order, with the roofline group
+        # of each: tools/prof_summary.py aligns them with a --pmc pass's dispatches to give
+        # each group its measured HBM bytes per call (roofline.traffic)
+        with open(os.environ["PG_BENCH_LAUNCHES"], "w") as f:
+            json.dump([dict(group=f"{fam}/{bound}", H=H, flops=fl, bytes=by)
+                       for fam, H, fl, by, ms, bound in timer._launches()], f)
 
     if rank == 0:
         roof = None
@@ -381,7 +402,9 @@ def main():
                                 for k, v in sorted(ksum.items())},
                         per_resolution=timer.per_resolution())
         cpu = None
+        log(f"timed: {1e3 * dt / args.steps:.3f} ms/step")
         if args.cpu_baseline == "auto" and world == 1:
+            log(f"CPU baseline: one oracle step on {args.cpu_threads or host_threads()} threads")
             cpu = cpu_baseline(args)
         line = {
             "metric": METRIC,

@@ -265,6 +265,19 @@ int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream)
 /* dtype conversion helpers */
 int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void* stream);
 
+/* ---- step plan: the kernel path of every 3x3 conv pass (forward, input
+ * gradient, weight gradient) of one train_step at (stage, batch, dtype) -- the layer list of
+ * pggan/nets.py:53-119 (G) and :164-239 (D) at scale_index = stage -- and the split-reduction
+ * workspace the step needs (the max over its conv / wgrad launches).  Plans are immutable
+ * after creation (thread-safe to read); the caller owns the workspace memory. */
+typedef struct pg_step_plan pg_step_plan;
+int pg_step_plan_create(int dtype, int n_depths, const int* depths, int stage, int batch,
+                        pg_step_plan** out);
+size_t pg_step_plan_workspace_size(const pg_step_plan* plan);
+/* human-readable table of the plan (one line per conv layer) into buf */
+int pg_step_plan_describe(const pg_step_plan* plan, char* buf, size_t len);
+void pg_step_plan_destroy(pg_step_plan* plan);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,6 +103,11 @@ _SIGS = {
     "pg_adam": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _F, _I, _VP], _I),
     "pg_randn": ([_SZ, _U64, _U64, _VP, _VP], _I),
     "pg_cast": ([_I, _I, _SZ, _VP, _VP, _VP], _I),
+    "pg_step_plan_create": ([_I, _I, ctypes.POINTER(ctypes.c_int), _I, _I,
+                             ctypes.POINTER(ctypes.c_void_p)], _I),
+    "pg_step_plan_workspace_size": ([_VP], _SZ),
+    "pg_step_plan_describe": ([_VP, ctypes.c_char_p, _SZ], _I),
+    "pg_step_plan_destroy": ([_VP], None),
 }
 SYMBOLS = ["pg_last_error"] + list(_SIGS)
 
@@ -156,6 +161,21 @@ class HipOps:
 
     def _dt(self, t):
         return PG_F32 if t.dtype == torch.float32 else PG_BF16
+
+    # -- step plan ---------------------------------------------------------
+    def step_plan(self, depths, stage, batch):
+        """(workspace bytes, description) of pg_step_plan_create for one training step."""
+        arr = (ctypes.c_int * len(depths))(*depths)
+        h = ctypes.c_void_p()
+        self._chk(self.lib.pg_step_plan_create(self.dt, len(depths), arr, stage, batch,
+                                               ctypes.byref(h)), "step_plan_create")
+        try:
+            ws = int(self.lib.pg_step_plan_workspace_size(h))
+            buf = ctypes.create_string_buffer(16384)
+            self._chk(self.lib.pg_step_plan_describe(h, buf, len(buf)), "step_plan_describe")
+            return ws, buf.value.decode()
+        finally:
+            self.lib.pg_step_plan_destroy(h)
 
     # -- conv ------------------------------------------------------------
     def packed_elems(self, mode, cout, cin):

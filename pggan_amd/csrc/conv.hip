@@ -1769,3 +1769,113 @@ int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale,
 }
 
 }  // extern "C"
+
+// --------------------------------------------------------------------------
+// Step plan: every 3x3 conv of G and D at one (stage, batch, dtype) with
+// the kernel path each pass takes and the split-reduction workspace the step needs.
+// Reference: the layer list of pggan/nets.py:53-119 (G), :164-239 (D) at scale_index.
+namespace {
+struct PlanLayer {
+  char net, kind[8];
+  int H, cin, cout, ups;
+  int fwd_path, dgrad_path;   // 0 conv3x3 (split-K when ws > 0), 1 conv_hr tile t, 2 conv_lr
+  int fwd_tile, dgrad_tile;
+  size_t fwd_ws, dgrad_ws, wgrad_ws;
+  int wg_MO, wg_WNC, wg_splits;
+};
+}  // namespace
+
+struct pg_step_plan {
+  int dtype, stage, batch;
+  size_t ws_bytes;
+  int n;
+  PlanLayer layers[64];
+};
+
+namespace {
+void plan_conv(int dtype, pg_conv_desc* d, int* path, int* tile, size_t* ws) {
+  *ws = conv_ws_bytes(d);
+  *path = 0;
+  *tile = -1;
+  if (dtype == PG_BF16) {
+    if (conv_lr_ok(d)) { *path = 2; *ws = 0; return; }
+    if (conv_hr_ok(d)) { *path = 1; *tile = conv_hr_tile(d); *ws = 0; }
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int pg_step_plan_create(int dtype, int n_depths, const int* depths, int stage, int batch,
+                        pg_step_plan** out) {
+  PG_CHECK_ARG(out && depths && stage >= 0 && stage + 1 <= n_depths && batch > 0 &&
+                   (dtype == PG_F32 || dtype == PG_BF16),
+               "step_plan_create: bad arguments");
+  pg_step_plan* p = new pg_step_plan();
+  p->dtype = dtype; p->stage = stage; p->batch = batch; p->ws_bytes = 0; p->n = 0;
+  auto add = [&](char net, const char* kind, int H, int cin, int cout, int ups) {
+    PlanLayer& L = p->layers[p->n++];
+    L.net = net;
+    snprintf(L.kind, sizeof(L.kind), "%s", kind);
+    L.H = H; L.cin = cin; L.cout = cout; L.ups = ups;
+    pg_conv_desc d{};
+    d.B = batch; d.H = d.W = H; d.cin = cin; d.cout = cout;
+    d.x_cs = cinp_of(cin); d.y_cs = (cout + 3) & ~3; d.flags = ups ? PG_CONV_UPS_IN : 0;
+    plan_conv(dtype, &d, &L.fwd_path, &L.fwd_tile, &L.fwd_ws);
+    pg_conv_desc g = d;   // input gradient: the transposed conv, cout -> cin channels
+    g.cin = cout; g.cout = (cin + 3) & ~3; g.x_cs = cinp_of(cout); g.y_cs = g.cout; g.flags = 0;
+    plan_conv(dtype, &g, &L.dgrad_path, &L.dgrad_tile, &L.dgrad_ws);
+    L.wgrad_ws = dtype == PG_BF16 ? wgrad_bf16_ws_bytes(&d) : 0;
+    if (dtype == PG_BF16) {
+      const WgbPlan w = wgrad_bf16_plan(&d);
+      L.wg_MO = w.MO; L.wg_WNC = w.WNC; L.wg_splits = w.splits;
+    } else {
+      L.wg_MO = L.wg_WNC = 0; L.wg_splits = 1;
+    }
+    p->ws_bytes = std::max({p->ws_bytes, L.fwd_ws, L.dgrad_ws, L.wgrad_ws});
+  };
+  const int d0 = depths[0];
+  add('G', "first", 4, d0, d0, 0);
+  for (int i = 0; i < stage; ++i) {
+    const int R = 8 << i;
+    add('G', "a", R, depths[i], depths[i + 1], 1);
+    add('G', "b", R, depths[i + 1], depths[i + 1], 0);
+  }
+  add('D', "mb", 4, d0 + 1, d0, 0);
+  for (int i = 0; i < stage; ++i) {
+    const int R = 8 << i;
+    add('D', "a", R, depths[i + 1], depths[i + 1], 0);
+    add('D', "b", R, depths[i + 1], depths[i], 0);
+  }
+  *out = p;
+  return PG_OK;
+}
+
+size_t pg_step_plan_workspace_size(const pg_step_plan* plan) { return plan ? plan->ws_bytes : 0; }
+
+int pg_step_plan_describe(const pg_step_plan* plan, char* buf, size_t len) {
+  PG_CHECK_ARG(plan && buf && len > 0, "step_plan_describe: bad arguments");
+  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr"};
+  size_t o = 0;
+  auto put = [&](const char* fmt, auto... a) {
+    if (o < len) o += snprintf(buf + o, len - o, fmt, a...);
+  };
+  put("stage %d batch %d dtype %s workspace %zu bytes\n", plan->stage, plan->batch,
+      plan->dtype == PG_BF16 ? "bf16" : "f32", plan->ws_bytes);
+  for (int i = 0; i < plan->n; ++i) {
+    const PlanLayer& L = plan->layers[i];
+    put("%c %-5s %4dx%-4d %3d->%-3d%s fwd %s", L.net, L.kind, L.H, L.H, L.cin, L.cout,
+        L.ups ? " up2" : "    ", path[L.fwd_path]);
+    if (L.fwd_path == 1) put("/t%d", L.fwd_tile);
+    if (L.fwd_ws) put("/splitK");
+    put("  dgrad %s", path[L.dgrad_path]);
+    if (L.dgrad_path == 1) put("/t%d", L.dgrad_tile);
+    if (L.dgrad_ws) put("/splitK");
+    put("  wgrad MO%d WNC%d splits %d\n", L.wg_MO, L.wg_WNC, L.wg_splits);
+  }
+  return PG_OK;
+}
+
+void pg_step_plan_destroy(pg_step_plan* plan) { delete plan; }
+
+}  // extern "C"

@@ -185,6 +185,13 @@ class StepEngine:
         self.fuse_pnbwd = os.environ.get("PG_PNBWD", "1") != "0"
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
+        self.plan = None        # pg_step_plan description (HIP library)
+        if forward_only is None and hasattr(ops, "step_plan"):
+            # the step's split-reduction workspace at once (pg_step_plan_workspace_size), so
+            # no launch of the step allocates
+            need, self.plan = ops.step_plan(self.depths, s, B)
+            if need:
+                self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
         # alpha == 1: the low-resolution branches of the fade-in (toRGB / fromRGB of the
         # previous level, the real-image fade) are multiplied by exactly 0 in the reference
         # (pggan/nets.py:155-156,263-265, pggan/model.py:217-221) and contribute exactly 0 to

@@ -34,14 +34,16 @@ for step in "$@"; do
       ROOT=$(pwd)
       export TMPDIR=/tmp
       for c in FETCH_SIZE WRITE_SIZE; do
-        ( cd /tmp && timeout -k 10 900 rocprofv3 --pmc $c --output-format csv \
+        rm -rf "gpurun_out/pmc_$c"
+        ( cd /tmp && PG_BENCH_LAUNCHES="$ROOT/gpurun_out/launches_$c.json" timeout -k 10 900 \
+            rocprofv3 --pmc $c --output-format csv \
             -d "$ROOT/gpurun_out/pmc_$c" -o run -- python "$ROOT/bench.py" --steps 1 --warmup 1 \
-            --cpu-baseline off --no-kernel-events ) > gpurun_out/pmc_$c.log 2>&1
+            --cpu-baseline off ) > gpurun_out/pmc_$c.log 2>&1
         rc=$?; echo "pmc $c rc=$rc"; tail -n 3 gpurun_out/pmc_$c.log
         if [ $rc -ne 0 ]; then exit $rc; fi
       done
       python tools/prof_summary.py gpurun_out/prof --fetch gpurun_out/pmc_FETCH_SIZE \
-        --write gpurun_out/pmc_WRITE_SIZE \
+        --write gpurun_out/pmc_WRITE_SIZE --launches gpurun_out/launches_FETCH_SIZE.json \
         -o gpurun_out/prof_summary.json > /dev/null ;;
     shapes) PG_BENCH_SHAPES=gpurun_out/shapes.json run shapes 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
     wg) run wg 600 python -m pytest tests/test_gpu_ops.py -q -x -k wgrad ;;

@@ -20,13 +20,57 @@ from collections import defaultdict
 
 
 def family(name):
-    if "conv3x3_kernel" in name or "conv_hr_kernel" in name:
+    if "conv3x3_kernel" in name or "conv_hr_kernel" in name or "conv_lr_kernel" in name:
         return "conv3x3", True
     if "conv_splitk_epilogue" in name:
         return "conv3x3", False
     if "wgrad3x3_kernel" in name or "wgrad_bf16_kernel" in name:
         return "wgrad3x3", True
+    if "wgrad_slab_reduce" in name:
+        return "wgrad3x3", False
     return None, False
+
+
+def group_traffic(path_fetch, path_write, launches_json):
+    """HBM bytes per call of each (family, bound) roofline group of bench.py: the last N
+    conv / wgrad calls of each --pmc pass (N = the instrumented step's calls, every step
+    launches the same sequence) aligned one to one with bench.py's launch list; a call =
+    its main kernel + the split epilogue / slab reduction that follows it."""
+    launches = json.load(open(launches_json))
+    n = len(launches)
+
+    def calls(path, counter):
+        path = _resolve(path, "counter_collection.csv")
+        rows = []
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r.get("Counter_Name") != counter:
+                    continue
+                fm, is_call = family(r["Kernel_Name"])
+                if fm:
+                    rows.append((int(r.get("Dispatch_Id") or r.get("Correlation_Id") or 0),
+                                 fm, is_call, float(r["Counter_Value"])))
+        rows.sort()
+        out = []
+        for _, fm, is_call, v in rows:
+            if is_call or not out:
+                out.append([fm, 0.0])
+            out[-1][1] += v
+        return out[-n:]
+
+    fe, wr = calls(path_fetch, "FETCH_SIZE"), calls(path_write, "WRITE_SIZE")
+    assert len(fe) == n and len(wr) == n, (len(fe), len(wr), n)
+    groups = defaultdict(lambda: dict(calls=0, hbm_bytes=0.0, alg_bytes=0.0))
+    for L, (f1, fv), (f2, wv) in zip(launches, fe, wr):
+        assert L["group"].split("/")[0] == f1 == f2, (L["group"], f1, f2)
+        g = groups[L["group"]]
+        g["calls"] += 1
+        g["hbm_bytes"] += (2.0 * fv + wv) * 1024.0
+        g["alg_bytes"] += L["bytes"]
+    return {k: dict(calls=v["calls"], hbm_bytes_per_call=v["hbm_bytes"] / v["calls"],
+                    alg_bytes_per_call=v["alg_bytes"] / v["calls"],
+                    traffic_over_alg=v["hbm_bytes"] / max(v["alg_bytes"], 1.0))
+            for k, v in groups.items()}
 
 
 def short(name):
@@ -109,6 +153,7 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("-o", "--out")
+    ap.add_argument("--launches", help="bench.py PG_BENCH_LAUNCHES dump of the PMC runs")
     ap.add_argument("--config", default="stage8_b4_bf16",
                     help="bench.py workload key the profiled run used (bench.py matches it)")
     a = ap.parse_args()
@@ -131,6 +176,8 @@ def main():
                                              write=wper.get(n, [0, 1])[0] / max(wper.get(n, [0, 1])[1], 1),
                                              dispatches=f[1])
                                      for n, f in sorted(fper.items(), key=lambda kv: -kv[1][0])[:25]}
+        if a.launches:
+            res["groups"] = group_traffic(a.fetch, a.write, a.launches)
         res["pmc_note"] = ("bytes/call = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 summed over the "
                            "family's dispatches of the PMC passes / the family's calls; "
                            "calibrate with adam_kernel: 28 B per parameter (4 fp32 reads, 3 writes)")
