@@ -3,8 +3,8 @@
 # other than pass (0) / test failures (1).  Logs and outputs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-PG_PARITY_OUT=gpurun_out/parity timeout -k 10 1500 python -u -m pytest tests -m gpu -q \
-  --timeout 900 --timeout-method thread > gpurun_out/gpu_all.log 2>&1
+PG_PARITY_OUT=gpurun_out/parity timeout -k 10 780 python -u -m pytest tests -m gpu -q \
+  --timeout 300 --timeout-method thread > gpurun_out/gpu_all.log 2>&1
 rc=$?; echo "gpu tests rc=$rc"; tail -n 3 gpurun_out/gpu_all.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
