@@ -46,6 +46,7 @@ struct ConvParams {
   const unsigned char* xbits;
   int xb_cs;
   int lg_tx, lg_ty;   // conv_hr: log2 of the tile counts along x and y
+  int xcd_remap;      // conv3x3_kernel: XCD-aware workgroup order
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
@@ -118,13 +119,27 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const int wm = wid / WN, wn = wid % WN;
   const int g = lane >> 4, r = lane & 15;
 
-  int t = blockIdx.x;
+  // XCD-aware block order (as in wgrad_bf16_kernel): every XCD owns a contiguous range of
+  // logical (tile, cout block, K chunk) ids, so the workgroups that share a K chunk's
+  // weights and halos run behind one L2 instead of pulling them through all eight
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd_remap) {
+    const int ox = gridDim.x, oy = gridDim.y;
+    const int n = ox * oy * gridDim.z;
+    const int h = bx + ox * (by + oy * bz);
+    const int xcd = h & 7, slot = h >> 3, q = n >> 3, rr = n & 7;
+    const int Lg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+    bx = Lg % ox;
+    by = (Lg / ox) % oy;
+    bz = Lg / (ox * oy);
+  }
+  int t = bx;
   const int tx0 = (t % p.tiles_x) * cTW;
   t /= p.tiles_x;
   const int ty0 = (t % p.tiles_y) * cTH;
   t /= p.tiles_y;
   const int b0 = t * cNB;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = by * BN;
 
   const int TW2 = cTW + 2;
   const int HW2 = (cTH + 2) * TW2;
@@ -197,7 +212,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
     }
   };
 
-  const int ch_begin = blockIdx.z * p.cps;
+  const int ch_begin = bz * p.cps;
   const int ch_end = min(p.nchunks, ch_begin + p.cps);
   if (ch_begin < ch_end) prefetch(ch_begin * cCK);
   for (int ch = ch_begin; ch < ch_end; ++ch) {
@@ -309,7 +324,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
         }
         if (p.ws) {
           if (b < p.B && n < p.cout_p)
-            *reinterpret_cast<f32x4_t*>(p.ws + blockIdx.z * p.slab + pix * p.cout_p + n) =
+            *reinterpret_cast<f32x4_t*>(p.ws + bz * p.slab + pix * p.cout_p + n) =
                 f32x4_t{v[0], v[1], v[2], v[3]};
           continue;
         }
@@ -407,7 +422,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const bool do_acc = (p.flags & PG_CONV_ACCUM) != 0;
   T* y = reinterpret_cast<T*>(p.y);
   if (p.ws) {   // split-K partial: raw fp32 sums to this split's slab, [pixel][cout_p]
-    float* slab = p.ws + blockIdx.z * p.slab;
+    float* slab = p.ws + bz * p.slab;
     for (int i = tid; i < BM * NV; i += 256) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
@@ -766,6 +781,7 @@ struct WgBParams {
   const unsigned char* gzb;
   int gzb_cs;
   float slope;
+  int xcd_remap;      // XCD-aware workgroup order (see the kernel prologue)
 };
 
 // pixels per staged tile: 128, or 256 (16x16) for the wide tiles at W >= 16 (half the
@@ -801,7 +817,22 @@ void wgrad_bf16_kernel(WgBParams p) {
   const int wk = wid % KW, wmn = wid / KW;
   const int wo = wmn / WNC, wc = wmn % WNC;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, pq = i16 & 3;
-  const int o0 = blockIdx.x * BO, c0 = blockIdx.y * BC;
+  // XCD-aware block order: consecutive workgroups go to different XCDs (8, round robin),
+  // so the ot x ct workgroups of one pixel split (which stage the same gz / x tiles) would
+  // each pull them through a different L2.  Remap so every XCD owns a contiguous range of
+  // logical ids (bijective for any grid size): a split's workgroups share one L2.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd_remap) {
+    const int ox = gridDim.x, oy = gridDim.y;
+    const int n = ox * oy * gridDim.z;
+    const int h = bx + ox * (by + oy * bz);
+    const int xcd = h & 7, slot = h >> 3, q = n >> 3, rr = n & 7;
+    const int L = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+    bx = L % ox;
+    by = (L / ox) % oy;
+    bz = L / (ox * oy);
+  }
+  const int o0 = bx * BO, c0 = by * BC;
   const int TW2 = p.TW + 2, HW2 = (p.TH + 2) * TW2;
   const int nhalo = p.halo_elems * HV;
 
@@ -813,7 +844,7 @@ void wgrad_bf16_kernel(WgBParams p) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[a][b][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const bool do_db = p.db && blockIdx.y == 0;
+  const bool do_db = p.db && by == 0;
   float bs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bs[e] = 0.f;
@@ -990,7 +1021,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   u32x4_t rg[PD][NGZ], rh[PD][NH];
   int rb[PD][NGZ];
   unsigned gokr[PD], hokr[PD];
-  const int t_begin = blockIdx.z * p.tiles_per_split;
+  const int t_begin = bz * p.tiles_per_split;
   const int t_end = min(p.ntiles, t_begin + p.tiles_per_split);
   // tiles past the end re-load the last tile (never stored): no branch around the loads
 #pragma unroll
@@ -1022,7 +1053,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       for (int r = v; r < 256; r += GV) s += red[r * 8 + e];
       const int o = o0 + tid;
       if (p.mode == WG_SLABS)
-        p.ws[blockIdx.z * p.slab + (size_t)p.cout * p.cin * 9 + o] = s;
+        p.ws[bz * p.slab + (size_t)p.cout * p.cin * 9 + o] = s;
       else   // WG_DIRECT: sole writer, one add like a read-modify-write (see the dW epilogue)
         atomicAdd(p.db + o, s * p.scale);
     }
@@ -1030,7 +1061,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   // ---- epilogue, one (mo, nc) 16x16x9 block per round: every wave dumps its partial
   // accumulators to LDS ([wave][tap][lane][j]); all 256 threads then sum the KW
   // partials of each (o, c, tap) and write [o][c][tap] runs contiguously.
-  float* slab = p.mode == WG_SLABS ? p.ws + blockIdx.z * p.slab : nullptr;
+  float* slab = p.mode == WG_SLABS ? p.ws + bz * p.slab : nullptr;
 #pragma unroll 1
   for (int r = 0; r < MO * NC; ++r) {
     const int a = r / NC, b = r % NC;
@@ -1192,6 +1223,8 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.gzb = (d->flags & PG_CONV_GZ_BITS) ? reinterpret_cast<const unsigned char*>(gzbits) : nullptr;
   p.gzb_cs = d->xb_cs;
   p.slope = d->slope;
+  static const int xcd = getenv("PG_WG_XCD") ? atoi(getenv("PG_WG_XCD")) : 1;   // A/B switch
+  p.xcd_remap = xcd;
   PG_CHECK_ARG(!p.gzb || (d->xb_cs * 8 >= d->cout && pl.tc.TH % 2 == 0 && pl.tc.TW % 2 == 0),
                "wgrad_bf16: GZ_BITS needs gzbits with >= cout/8 bytes per pixel");
   PG_CHECK_ARG(pl.BP == BP && p.halo_elems <= wgb_maxhalo(BP), "wgrad_bf16: halo %d > %d", p.halo_elems,
@@ -1477,6 +1510,8 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.ws = splits > 1 ? (float*)ws : nullptr;
   p.cps = pg_cdiv(p.nchunks, splits);
   p.slab = (size_t)d->B * d->H * d->W * p.cout_p;
+  static const int xcd = getenv("PG_CONV_XCD") ? atoi(getenv("PG_CONV_XCD")) : 1;   // A/B switch
+  p.xcd_remap = xcd;
   dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
             splits);
   static bool attr_done = false;
