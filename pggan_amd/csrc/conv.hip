@@ -792,9 +792,16 @@ constexpr int wgb_maxhalo(int bp) { return bp == 128 ? 288 : 18 * 18; }   // pic
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
+#ifndef PG_WG_PRE_ALL
+#define PG_WG_PRE_ALL 1
+#endif
 template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB, int BP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 void wgrad_bf16_kernel(WgBParams p) {
+  // precomputed per-lane staging offsets + shifts for the tile origin (every tile when
+  // PG_WG_PRE_ALL; the 64-bit per-load address math of the other form put each wide-tile
+  // halo load behind its own branch, ~600 instructions of staging per 72 MFMAs)
+  constexpr bool PRE = PG_WG_PRE_ALL || MO < 4;
   constexpr int KW = 4 / (WMO * WNC);
   constexpr int BO = WMO * MO * 16, BC = WNC * NC * 16;
   constexpr int GV = BO / 8, HV = BC / 8;
@@ -879,7 +886,7 @@ void wgrad_bf16_kernel(WgBParams p) {
     // upsample's floor shift splits: (t0 + h - 1) >> 1 = t0 / 2 + ((h - 1) >> 1))
     const int pk = hpk[k] < 0 ? 0 : hpk[k];
     const int ys = p.ups ? 1 : 0;
-    if constexpr (MO < 4) hrel[k] = (((pk >> 24) * p.Hin + ((((pk >> 16) & 0xff) - 1) >> ys)) * p.Win +
+    if constexpr (PRE) hrel[k] = (((pk >> 24) * p.Hin + ((((pk >> 16) & 0xff) - 1) >> ys)) * p.Win +
                ((((pk >> 8) & 0xff) - 1) >> ys)) * p.x_cs + 8 * (pk & 0xff);
   }
   // ok masks of a loaded tile: bit k of gz vector k / halo vector k (zero fill at the
@@ -887,7 +894,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   auto load_tile = [&](int t, u32x4_t (&rg)[NGZ], u32x4_t (&rh)[NH], int (&rb)[NGZ],
                        unsigned& gok, unsigned& hok) {
     // tile -> origin (wave-uniform, scalar; shifts where the tile counts are powers of 2)
-    constexpr bool sh = MO < 4;   // A/B: shifts help the narrow tiles, not the wide ones
+    constexpr bool sh = PRE;
     const int tx0 = (sh && p.lg_tx >= 0 ? (t & (p.tiles_x - 1)) : t % p.tiles_x) * p.TW;
     const int tt = sh && p.lg_tx >= 0 ? t >> p.lg_tx : t / p.tiles_x;
     const int ty0 = (sh && p.lg_ty >= 0 ? (tt & (p.tiles_y - 1)) : tt % p.tiles_y) * p.TH;
@@ -908,7 +915,7 @@ void wgrad_bf16_kernel(WgBParams p) {
     }
     const int ys = p.ups ? 1 : 0;
     // the tile's input origin (scalar) + the lane's precomputed offset
-    const bf16_t* xt = MO < 4 ? p.x + c0 + (((size_t)b0 * p.Hin + (ty0 >> ys)) * p.Win + (tx0 >> ys)) * p.x_cs
+    const bf16_t* xt = PRE ? p.x + c0 + (((size_t)b0 * p.Hin + (ty0 >> ys)) * p.Win + (tx0 >> ys)) * p.x_cs
                               : p.x;
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
@@ -916,7 +923,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int yy = ty0 + ((pk >> 16) & 0xff) - 1, xx = tx0 + ((pk >> 8) & 0xff) - 1;
       const bool ok = pk >= 0 && b0 + (pk >> 24) < p.B && (unsigned)yy < (unsigned)p.H &&
                       (unsigned)xx < (unsigned)p.W;
-      if constexpr (MO < 4) {   // precomputed offsets (A/B: -7..-13 % at 1024^2)
+      if constexpr (PRE) {   // precomputed offsets (A/B: -7..-13 % at 1024^2)
         rh[k] = *reinterpret_cast<const u32x4_t*>(ok ? xt + hrel[k] : p.x);
       } else {                  // wide tiles: registers are tighter than VALU (+2 % the other way)
         rh[k] = *reinterpret_cast<const u32x4_t*>(

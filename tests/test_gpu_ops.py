@@ -71,6 +71,10 @@ CONV_CASES = [
     (4, 512, 16, 16, ("bias", "lrelu")),        # > 2048 tiles: several tiles per workgroup
     (4, 512, 32, 16, ("mask",)),
     (4, 512, 16, 32, ("ups", "bias", "lrelu", "pool")),
+    # wide 8-wave tile (conv_hr tile 3, LDS-DMA double-buffered staging): >= 256 tiles
+    (4, 128, 64, 128, ("bias", "lrelu")),
+    (8, 128, 64, 64, ("ups", "bias", "lrelu", "pool")),
+    (4, 128, 128, 128, ("mask", "accum")),
 ]
 
 
