@@ -820,6 +820,7 @@ void wgrad_bf16_kernel(WgBParams p) {
   auto grow = [](int r) { return r * GZS + (r >> 3) * 64; };
   auto hrow = [hpad](int r) { return r * HS + (r >> 3) * hpad; };
   bf16_t* hal = gzl + grow(BP);
+  const int hscr = hrow(p.halo_elems);   // 16-B scratch slot behind the halo (see store_tile)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wk = wid % KW, wmn = wid / KW;
   const int wo = wmn / WNC, wc = wmn % WNC;
@@ -963,12 +964,13 @@ void wgrad_bf16_kernel(WgBParams p) {
     }
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
+      // branch-free: lanes past the halo write a scratch slot behind it (an exec-masked
+      // store block here made the compiler drain every prefetched tile, vmcnt(0), once per
+      // PD tiles)
       const int i = tid + k * 256;
-      if (i < nhalo) {
-        const int hp = i / HV, v = i - hp * HV;
-        *reinterpret_cast<u32x4_t*>(hal + hrow(hp) + 8 * v) =
-            ((hok >> k) & 1u) ? rh[k] : u32x4_t{0u, 0u, 0u, 0u};
-      }
+      const int hp = i / HV, v = i - hp * HV;
+      const int off = i < nhalo ? hrow(hp) + 8 * v : hscr;
+      *reinterpret_cast<u32x4_t*>(hal + off) = ((hok >> k) & 1u) ? rh[k] : u32x4_t{0u, 0u, 0u, 0u};
     }
   };
   // halo rows of this lane's two k-rows for each k-step the wave owns (tile-invariant)
@@ -1034,16 +1036,19 @@ void wgrad_bf16_kernel(WgBParams p) {
 #pragma unroll
   for (int d = 0; d < PD; ++d)
     load_tile(min(t_begin + d, t_end - 1), rg[d], rh[d], rb[d], gokr[d], hokr[d]);
+  // the staging stores and loads run unconditionally (tiles past the end store zeros and
+  // skip their MFMAs), so the compiler's load counting stays exact across the back edge
+  // and PD tiles of loads really stay in flight (a branch around them cost a full vmcnt(0)
+  // drain per PD tiles)
   for (int t = t_begin; t < t_end; t += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
-      if (t + d < t_end) {
-        __syncthreads();   // the previous tile's fragments have been read
-        store_tile(rg[d], rh[d], rb[d], gokr[d], hokr[d]);
-        __syncthreads();
-        load_tile(min(t + d + PD, t_end - 1), rg[d], rh[d], rb[d], gokr[d], hokr[d]);
-        compute_tile();
-      }
+      const bool live = t + d < t_end;
+      __syncthreads();   // the previous tile's fragments have been read
+      store_tile(rg[d], rh[d], rb[d], live ? gokr[d] : 0u, live ? hokr[d] : 0u);
+      __syncthreads();
+      load_tile(min(t + d + PD, t_end - 1), rg[d], rh[d], rb[d], gokr[d], hokr[d]);
+      if (live) compute_tile();   // no global memory access inside: the counting stays exact
     }
   }
 
@@ -1066,14 +1071,17 @@ void wgrad_bf16_kernel(WgBParams p) {
     }
   }
   // ---- epilogue, one (mo, nc) 16x16x9 block per round: every wave dumps its partial
-  // accumulators to LDS ([wave][tap][lane][j]); all 256 threads then sum the KW
-  // partials of each (o, c, tap) and write [o][c][tap] runs contiguously.
+  // accumulators to LDS in output order ([wave][o][c][tap]: the lane's 16x16 MFMA
+  // fragment holds c = lane & 15, o = 4 * (lane >> 4) + j); all 256 threads then sum the
+  // KW partials of each (o, c, tap) from consecutive words (conflict free; the former
+  // [tap][lane][j] image put the 9 taps a lane group reads 256 words apart, on one bank:
+  // ~45 % of the kernel's LDS cycles were conflicts) and write [o][c][tap] runs contiguously.
   float* slab = p.mode == WG_SLABS ? p.ws + bz * p.slab : nullptr;
 #pragma unroll 1
   for (int r = 0; r < MO * NC; ++r) {
     const int a = r / NC, b = r % NC;
     __syncthreads();
-    float* mine = red + (size_t)wid * (9 * 64 * 4);
+    float* mine = red + (size_t)wid * 2304 + ((lane >> 4) * 64 + (lane & 15)) * 9;
 #pragma unroll
     for (int mo = 0; mo < MO; ++mo)
 #pragma unroll
@@ -1081,7 +1089,8 @@ void wgrad_bf16_kernel(WgBParams p) {
         if (mo == a && nc == b) {
 #pragma unroll
           for (int t = 0; t < 9; ++t)
-            *reinterpret_cast<f32x4_t*>(mine + (t * 64 + lane) * 4) = acc[mo][nc][t];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mine[j * 16 * 9 + t] = acc[mo][nc][t][j];
         }
     __syncthreads();
     constexpr int NOUT = (4 / KW) * 2304;   // outputs of this round (per wmn: 16 o x 16 c x 9)
@@ -1094,10 +1103,9 @@ void wgrad_bf16_kernel(WgBParams p) {
       const int m = e / 2304, rem = e - m * 2304;
       const int ol = rem / 144, rem2 = rem - ol * 144;
       const int cl = rem2 / 9, tap = rem2 - cl * 9;
-      const int src = ((tap * 64 + (ol >> 2) * 16 + cl) * 4) + (ol & 3);
       float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < KW; ++k) sum += red[(size_t)(m * KW + k) * (9 * 64 * 4) + src];
+      for (int k = 0; k < KW; ++k) sum += red[(size_t)(m * KW + k) * 2304 + rem];
       const int mwo = m / WNC, mwc = m % WNC;
       const int o = o0 + (mwo * MO + a) * 16 + ol;
       const int c = c0 + (mwc * NC + b) * 16 + cl;
@@ -1246,7 +1254,8 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   } else {
     p.mode = WG_ATOMIC;
   }
-  int lds = (BP * p.GZS + (BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2;
+  // + 16 B: store_tile's scratch slot behind the halo
+  int lds = (BP * p.GZS + (BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2 + 16;
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
@@ -1311,6 +1320,8 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_WGB(1, 1, 1, 2, 2, 2)
   PG_WGB(2, 1, 1, 1, 2, 2)
   PG_WGB(2, 1, 1, 2, 2, 2)
+  PG_WGB(2, 1, 1, 2, 2, 1)
+  PG_WGB(2, 1, 1, 2, 1, 2)
   PG_WGB(4, 1, 1, 1, 1, 2)
   PG_WGB(4, 1, 1, 1, 2, 2)
   PG_WGB(4, 1, 1, 1, 2, 1)

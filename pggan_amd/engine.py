@@ -205,6 +205,19 @@ class StepEngine:
         # grad_ready(net, names) right after the last kernel writing those gradients in the
         # final backward pass of a half-step, or None (DP bucketing, pggan_amd.dp)
         self.grad_ready = None
+        # weight gradients on a second stream (HIP device, training step): every conv wgrad
+        # of a backward pass is off the pass's critical path (the input-gradient chain), so it
+        # runs beside the next levels' convs -- at 4^2-32^2 neither launch fills the 256 CUs.
+        # One side stream serialises the wgrads among themselves, so every dW accumulates in
+        # the same order as on one stream (bitwise-equal results).  _join() orders the side
+        # stream back into the main one before anything overwrites a wgrad input or reads a
+        # gradient (see _side_join).  PG_SIDE_WGRAD=0 keeps one stream (A/B runs).
+        self.side = None
+        self._side_pending = set()
+        self.ws_side = None
+        if (forward_only is None and str(device).startswith("cuda") and
+                os.environ.get("PG_SIDE_WGRAD", "1") != "0"):
+            self.side = torch.cuda.Stream(device=device)
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -375,9 +388,8 @@ class StepEngine:
                          bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2,
                          ws=self.ws if need else None, **kw)
 
-    def _ws_need(self, kind, H, cin, cout, ups):
-        """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape); the
-        shared workspace grows to the largest need (launches are stream-ordered)."""
+    def _ws_bytes(self, kind, H, cin, cout, ups):
+        """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape)."""
         key = (kind, H, cin, cout, ups)
         need = self._ws_cache.get(key)
         if need is None:
@@ -387,6 +399,12 @@ class StepEngine:
                 need = self.ops.wgrad_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout,
                                                       ups=ups)
             self._ws_cache[key] = need
+        return need
+
+    def _ws_need(self, kind, H, cin, cout, ups):
+        """_ws_bytes, growing the main stream's shared workspace to the largest need
+        (launches on one stream are ordered)."""
+        need = self._ws_bytes(kind, H, cin, cout, ups)
         if need and (self.ws is None or self.ws.numel() * 4 < need):
             self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         return need
@@ -396,10 +414,32 @@ class StepEngine:
         """gzbits: gz is the pooled-resolution gradient g and the conv's output gradient is
         gscale * up2(g) * lrelu'(gzbits) (never materialised)."""
         c = self.packs[(net, key)][3]
-        need = self._ws_need("w", H, cin, cout, ups)
         kw = dict(gzbits=gzbits, slope=SLOPE) if gzbits is not None else {}
-        self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
-                            scale=c * gscale, db=db, ws=self.ws if need else None, **kw)
+        if self.side is None:
+            need = self._ws_need("w", H, cin, cout, ups)
+            self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
+                                scale=c * gscale, db=db, ws=self.ws if need else None, **kw)
+            return
+        need = self._ws_bytes("w", H, cin, cout, ups)
+        if need and (self.ws_side is None or self.ws_side.numel() * 4 < need):
+            self._side_join()   # the side stream may still read the old workspace
+            self.ws_side = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
+        # x and gz were written on the main stream: the side stream starts after them
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
+                                scale=c * gscale, db=db, ws=self.ws_side if need else None, **kw)
+        self._side_pending.add(net)
+
+    def _side_join(self, net=None):
+        """Order the pending side-stream weight gradients (all of them, or only if `net` has
+        some) before whatever the main stream enqueues next: called before a pass overwrites
+        a net's activation / gradient buffers, before Adam reads the gradients and at the
+        end of each half-step (so callers reading gradients need no stream handling)."""
+        if not self._side_pending or (net is not None and net not in self._side_pending):
+            return
+        torch.cuda.current_stream().wait_stream(self.side)
+        self._side_pending.clear()
 
     def _dbits(self, i):
         """Whether D level i keeps its conv-b (conv + lrelu + pool) output as sign bits only:
@@ -474,6 +514,7 @@ class StepEngine:
     def g_forward(self, P, z, alpha, keep=True):
         """keep: store what g_backward needs (the G half); the D half only needs the image."""
         ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
+        self._side_join("G")
         if z is not g["z"]:
             g["z"].copy_(z)
         ops.pixnorm(g["z"], g["zn"], self.latent)                            # nets.py:124-125
@@ -521,6 +562,7 @@ class StepEngine:
 
     def g_backward(self, P, GR, gimg, alpha):
         ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
+        self._side_join("G")
         kw = {}
         low = self._low(alpha)
         if low:
@@ -575,6 +617,7 @@ class StepEngine:
     # ================================================================== D
     def d_forward(self, P, img, alpha):
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        self._side_join("D")
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(img, P[fr.format(s) + "weight"], P[fr.format(s) + "bias"], he(3), D["yrgb"],
                      B=B, R=R, C=d[s], down=False, slope=SLOPE)            # nets.py:255
@@ -612,14 +655,25 @@ class StepEngine:
         return D["logit"]
 
     def _ready(self, net, *prefixes):
-        if self.grad_ready is not None:
-            self.grad_ready(net, [p + k for p in prefixes for k in ("weight", "bias")])
+        if self.grad_ready is None:
+            return
+        names = [p + k for p in prefixes for k in ("weight", "bias")]
+        if self.side is None:
+            self.grad_ready(net, names)
+            return
+        # the gradients come from both streams: the side stream waits for the main one and
+        # the callback runs on it, so a collective it starts sees both without stalling the
+        # main stream's next convs
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            self.grad_ready(net, names)
 
     def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False):
         """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
         gimg: accumulate dL/dimg (must be zeroed by the caller); keeps every gz.
         final: the last pass writing D's gradients this half-step (grad_ready calls)."""
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        self._side_join("D")
         ready = (lambda *p: self._ready("D", *p)) if final else (lambda *p: None)
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
@@ -712,6 +766,7 @@ class StepEngine:
         """Push gbar (= dR1/dx-gradient) forward through D with the B1 masks, adding the R1
         weight terms; returns (tangent logit, mbstd injection) for the B2 pass."""
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
+        self._side_join("D")
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(gbar, P[fr.format(s) + "weight"], None, he(3), D["trgb"], B=B, R=R, C=d[s],
                      down=False, slope=SLOPE, mask_y=D["yrgb"])
@@ -807,6 +862,7 @@ class StepEngine:
         self.d_backward(PD, GD, D["u"], alpha_D, img=img_fake, final=hp.gp_mode == "r1")
         if hp.gp_mode != "r1":
             self._wgan_gp(PD, GD, xr, img_fake, gp_eps, alpha_D)
+        self._side_join()
         return xr, img_fake
 
     def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
@@ -836,6 +892,7 @@ class StepEngine:
         D["gimg"].zero_()
         self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
         self.g_backward(PG, GG, D["gimg"], alpha_G)
+        self._side_join()
         return img
 
     def bind(self, fpG: FlatParams, fpD: FlatParams, hyper: Hyper):
@@ -852,6 +909,7 @@ class StepEngine:
 
     def adam(self, fp: FlatParams, lr):
         hp = self.hyper
+        self._side_join()
         fp.step += 1
         n = fp.n_live
         self.ops.adam(fp.flat[:n], fp.grad[:n], fp.m[:n], fp.v[:n], lr=lr, beta1=hp.beta1,

@@ -14,7 +14,7 @@ for d in sys.argv[1:]:
     agg = collections.defaultdict(list)
     info = {}
     for r in rows:
-        k = r["Kernel_Name"].split("(")[0][-60:]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-60:]
         agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
         info[k] = (r["Grid_Size"], r["VGPR_Count"], r["Accum_VGPR_Count"], r["LDS_Block_Size"])
     print(d)
