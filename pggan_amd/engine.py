@@ -213,11 +213,25 @@ class StepEngine:
         # stream back into the main one before anything overwrites a wgrad input or reads a
         # gradient (see _side_join).  PG_SIDE_WGRAD=0 keeps one stream (A/B runs).
         self.side = None
-        self._side_pending = set()
+        self._side_ev = {}      # buffer-set key -> last side-stream event reading it
         self.ws_side = None
+        self._dkey = "D"        # key of the D buffer set in use ("Df": the fake-image pass)
         if (forward_only is None and str(device).startswith("cuda") and
                 os.environ.get("PG_SIDE_WGRAD", "1") != "0"):
             self.side = torch.cuda.Stream(device=device)
+        # the fake-image pass of the D half (G forward, D forward + backward) depends on the
+        # real-image part (F, B1, R1, T, B2) only through the parameters, so it runs on its
+        # own stream beside it, with its own D buffer set, split-K workspace, weight-gradient
+        # stream and gradient buffer (summed into D's before Adam_D): the low-resolution
+        # launches of one pass (latency bound, a fraction of the CUs) share the GPU with the
+        # other pass's high-resolution ones.  Measured slower (A/B at C5: 311.0 -> 306.8 img/s,
+        # the two passes' high-resolution launches contend for HBM and the host enqueue grows
+        # 1.5 ms), so it is opt-in: PG_FAKE_STREAM=1.
+        self.fstream = self.side2 = None
+        self.ws_side2 = None
+        if self.side is not None and os.environ.get("PG_FAKE_STREAM", "0") == "1":
+            self.fstream = torch.cuda.Stream(device=device)
+            self.side2 = torch.cuda.Stream(device=device)
         self._alloc()
 
     # ------------------------------------------------------------------ buffers
@@ -259,7 +273,18 @@ class StepEngine:
             g["gh0"] = t(B, 4, 4, d[0])
             g["gzf"] = t(B, 4, 4, d[0])
         # ---- D
-        self.dd = D = {}
+        self.dd = self._alloc_D(need_D, train)
+        # the fake-image pass's buffer set (concurrent mode) and its split-K workspace
+        self.dd_f = self._alloc_D(need_D, train) if self.fstream is not None else None
+        self.ws_f = torch.empty_like(self.ws) if (self.fstream is not None and self.ws is not None) \
+            else None
+        # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
+        self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
+
+    def _alloc_D(self, need_D, train):
+        B, s, d, R = self.B, self.s, self.depths, self.R
+        t = self._t
+        D = {}
         if need_D:
             D["yrgb"] = t(B, R, R, d[s])
             if s >= 1:
@@ -316,8 +341,7 @@ class StepEngine:
             D["gp_norms"] = t(B, f32=True)
             D["ones"] = torch.full((B,), 1.0, dtype=torch.float32, device=self.dev)
             D["zeros"] = torch.zeros((B,), dtype=torch.float32, device=self.dev)
-        # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
-        self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        return D
 
     # ------------------------------------------------------------------ weights
     def _conv_list(self, net):
@@ -422,24 +446,42 @@ class StepEngine:
             return
         need = self._ws_bytes("w", H, cin, cout, ups)
         if need and (self.ws_side is None or self.ws_side.numel() * 4 < need):
-            self._side_join()   # the side stream may still read the old workspace
+            # the side stream may still read the old workspace
+            self.side.synchronize()
             self.ws_side = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
-        # x and gz were written on the main stream: the side stream starts after them
+        self._side_call((net,), self.ops.conv_wgrad, x, gz, dW, B=self.B, H=H, W=H, cin=cin,
+                        cout=cout, ups=ups, scale=c * gscale, db=db,
+                        ws=self.ws_side if need else None, **kw)
+
+    def _side_call(self, nets, fn, *a, **kw):
+        """Run a weight-gradient launch `fn` on the side stream (or inline without one).
+        nets: whose buffers it reads (joins before those are overwritten).  Its inputs were
+        written on the main stream, so the side stream first waits for it."""
+        if self.side is None:
+            return fn(*a, **kw)
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
-            self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
-                                scale=c * gscale, db=db, ws=self.ws_side if need else None, **kw)
-        self._side_pending.add(net)
+            fn(*a, **kw)
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        for n in nets:
+            self._side_ev[self._dkey if n == "D" else n] = ev
 
     def _side_join(self, net=None):
-        """Order the pending side-stream weight gradients (all of them, or only if `net` has
-        some) before whatever the main stream enqueues next: called before a pass overwrites
-        a net's activation / gradient buffers, before Adam reads the gradients and at the
-        end of each half-step (so callers reading gradients need no stream handling)."""
-        if not self._side_pending or (net is not None and net not in self._side_pending):
+        """Order the side-stream launches that read `net`'s buffers (all of them when None;
+        "D" = the D buffer set in use) before whatever the current stream enqueues next:
+        called before a pass overwrites a net's activation / gradient buffers, before Adam
+        reads the gradients and at the end of each half-step (so callers reading gradients
+        need no stream handling).  Events, not stream waits: a join never waits for side
+        work of the other buffer set."""
+        if not self._side_ev:
             return
-        torch.cuda.current_stream().wait_stream(self.side)
-        self._side_pending.clear()
+        keys = list(self._side_ev) if net is None else [self._dkey if net == "D" else net]
+        cur = torch.cuda.current_stream()
+        for k in keys:
+            ev = self._side_ev.pop(k, None)
+            if ev is not None:
+                cur.wait_event(ev)
 
     def _dbits(self, i):
         """Whether D level i keeps its conv-b (conv + lrelu + pool) output as sign bits only:
@@ -609,9 +651,10 @@ class StepEngine:
         self._ready("G", fb)
         self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)
         ops.pixnorm_lrelu_bwd(g["f"], g["gh0"], g["gzf"], d[0], self.hyper.slope_cfg)
-        ops.linear_wgrad(g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
-                         GR["latent_format_layer.module.bias"], B=B, flags=L.LIN_OUT_CHW,
-                         scale=he(self.latent))
+        self._side_call(("G",), ops.linear_wgrad,
+                        g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
+                        GR["latent_format_layer.module.bias"], B=B, flags=L.LIN_OUT_CHW,
+                        scale=he(self.latent))
         self._ready("G", "latent_format_layer.module.")
 
     # ================================================================== D
@@ -678,14 +721,16 @@ class StepEngine:
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
         if GR is not None:
-            ops.linear_wgrad(D["l1"], u, GR[dec + "weight"], GR[dec + "bias"], B=B, flags=0,
-                             scale=he(d[0]))
+            self._side_call(("D",), ops.linear_wgrad,
+                            D["l1"], u, GR[dec + "weight"], GR[dec + "bias"], B=B, flags=0,
+                            scale=he(d[0]))
             ready(dec)
         ops.linear_dgrad(u, P[dec + "weight"], D["gzl1"], B=B, flags=L.LIN_MASK, scale=he(d[0]),
                          slope=SLOPE, aux=D["l1"])
         if GR is not None:
-            ops.linear_wgrad(D["c"], D["gzl1"], GR[lin + "weight"], GR[lin + "bias"], B=B,
-                             flags=L.LIN_IN_CHW, scale=he(16 * d[0]))
+            self._side_call(("D",), ops.linear_wgrad,
+                            D["c"], D["gzl1"], GR[lin + "weight"], GR[lin + "bias"], B=B,
+                            flags=L.LIN_IN_CHW, scale=he(16 * d[0]))
             ready(lin)
         ops.linear_dgrad(D["gzl1"], P[lin + "weight"], D["gzc"], B=B,
                          flags=L.LIN_IN_CHW | L.LIN_MASK, scale=he(16 * d[0]), slope=SLOPE,
@@ -746,17 +791,20 @@ class StepEngine:
         fr = "fromRGB_blocks.{}.fromRGB.module."
         w = P[fr.format(s) + "weight"]
         if GR is not None:
-            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
-                             dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
+            # img may be the generator's output buffer (fake pass): pending for both nets
+            self._side_call(("D", "G"), ops.from_rgb_bwd,
+                            D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
+                            dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
             ready(fr.format(s))
         if gimg is not None:
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg)
         if low:
             w1 = P[fr.format(s - 1) + "weight"]
             if GR is not None:
-                ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True, img=img,
-                                 dw=GR[fr.format(s - 1) + "weight"],
-                                 db=GR[fr.format(s - 1) + "bias"])
+                self._side_call(("D", "G"), ops.from_rgb_bwd,
+                                D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True, img=img,
+                                dw=GR[fr.format(s - 1) + "weight"],
+                                db=GR[fr.format(s - 1) + "bias"])
                 ready(fr.format(s - 1))
             if gimg is not None:
                 ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True,
@@ -770,14 +818,16 @@ class StepEngine:
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(gbar, P[fr.format(s) + "weight"], None, he(3), D["trgb"], B=B, R=R, C=d[s],
                      down=False, slope=SLOPE, mask_y=D["yrgb"])
-        ops.from_rgb_bwd(D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
-                         down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
+        self._side_call(("D",), ops.from_rgb_bwd,
+                        D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
+                        down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
         low = self._low(alpha)
         if low:
             ops.from_rgb(gbar, P[fr.format(s - 1) + "weight"], None, he(3), D["td"], B=B, R=R // 2,
                          C=d[s - 1], down=True, slope=SLOPE, mask_y=D["yd"])
-            ops.from_rgb_bwd(D["gzd"], P[fr.format(s - 1) + "weight"], he(3), B=B, R=R // 2,
-                             C=d[s - 1], down=True, img=gbar, dw=GR[fr.format(s - 1) + "weight"])
+            self._side_call(("D",), ops.from_rgb_bwd,
+                            D["gzd"], P[fr.format(s - 1) + "weight"], he(3), B=B, R=R // 2,
+                            C=d[s - 1], down=True, img=gbar, dw=GR[fr.format(s - 1) + "weight"])
         t = D["trgb"]
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
@@ -813,11 +863,13 @@ class StepEngine:
         lin = "minibatch_normalization_block.linear.module."
         ops.linear(D["tc"], P[lin + "weight"], None, D["tl1"], B=B,
                    flags=L.LIN_IN_CHW | L.LIN_MASK, scale=he(16 * d[0]), slope=SLOPE, aux=D["l1"])
-        ops.linear_wgrad(D["tc"], D["gzl1"], GR[lin + "weight"], None, B=B, flags=L.LIN_IN_CHW,
-                         scale=he(16 * d[0]))
+        self._side_call(("D",), ops.linear_wgrad,
+                        D["tc"], D["gzl1"], GR[lin + "weight"], None, B=B, flags=L.LIN_IN_CHW,
+                        scale=he(16 * d[0]))
         dec = "decision_layer.module."
         ops.linear(D["tl1"], P[dec + "weight"], None, D["tout"], B=B, flags=0, scale=he(d[0]))
-        ops.linear_wgrad(D["tl1"], u, GR[dec + "weight"], None, B=B, flags=0, scale=he(d[0]))
+        self._side_call(("D",), ops.linear_wgrad,
+                        D["tl1"], u, GR[dec + "weight"], None, B=B, flags=0, scale=he(d[0]))
         return D["tout"], D["inj"]
 
     # ================================================================== step
@@ -830,6 +882,10 @@ class StepEngine:
         GD_flat.zero_()
         self.loss[:3].zero_()
         self.loss[4:5].zero_()
+        conc = self.fstream is not None and hp.gp_mode == "r1"
+        if conc:
+            ev0 = torch.cuda.Event()   # the fake pass starts from here, beside the real part
+            ev0.record(torch.cuda.current_stream())
         if self._low(alpha_D):
             ops.img_fade(real, alpha_D, D["real_in"])                       # :217-221
             xr = D["real_in"]
@@ -845,6 +901,9 @@ class StepEngine:
             tout, inj = self.d_tangent(PD, GD, D["gbar"], D["u"], alpha_D)
             ops.mul_add(D["u"], tout.view(-1), D["hl"], D["u2"])
             self.d_backward(PD, GD, D["u2"], alpha_D, img=xr, inj_mbstd=inj)
+            if conc:
+                img_fake = self._fake_pass_concurrent(PG, PD, z, alpha_G, alpha_D, ev0, before_fake)
+                return xr, img_fake
         else:
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
@@ -864,6 +923,44 @@ class StepEngine:
             self._wgan_gp(PD, GD, xr, img_fake, gp_eps, alpha_D)
         self._side_join()
         return xr, img_fake
+
+    def _fake_pass_concurrent(self, PG, PD, z, alpha_G, alpha_D, ev0, before_fake):
+        """The fake-image part of the D half on self.fstream with the second buffer set
+        (see __init__); its D gradients go to a second flat buffer that is added into D's
+        after both parts (per-parameter sums in a different order than the one-stream
+        schedule: within fp32 rounding).  The main stream waits for it on return."""
+        main, fs = torch.cuda.current_stream(), self.fstream
+        gd2 = self.__dict__.get("_gd2")
+        if gd2 is None or gd2[0] is not self.fpD:
+            buf = torch.zeros_like(self.fpD.grad)
+            gd2 = self._gd2 = (self.fpD, buf, {n: self.fpD._view(buf, n) for n in self.fpD.names})
+        _, buf, views = gd2
+        saved = (self.dd, self.ws, self.side, self.ws_side, self._dkey)
+        fs.wait_event(ev0)
+        with torch.cuda.stream(fs):
+            if before_fake is not None:
+                before_fake()      # a deferred Adam_G (+ G packing) only orders the G forward
+            self.dd, self.ws, self.side, self.ws_side, self._dkey = (
+                self.dd_f, self.ws_f, self.side2, self.ws_side2, "Df")
+            try:
+                D = self.dd
+                buf.zero_()
+                img_fake = self.g_forward(PG, z, alpha_G, keep=False)           # :226-227
+                if self.keep_fake_D:
+                    img_fake = img_fake.clone()
+                self.d_forward(PD, img_fake, alpha_D)                           # :228
+                self.ops.bce(D["logit"], False, 1.0, self.loss[1:2], D["u"], None)
+                # per-layer grad_ready is off here: the D gradient is final only after the sum
+                self.d_backward(PD, views, D["u"], alpha_D, img=img_fake, final=False)
+                self._side_join("D")
+            finally:
+                self.ws_f, self.ws_side2 = self.ws, self.ws_side
+                self.dd, self.ws, self.side, self.ws_side, self._dkey = saved
+        main.wait_stream(fs)
+        self._side_join()
+        n = self.fpD.n_live
+        self._GD_flat[:n].add_(buf[:n])
+        return img_fake
 
     def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
         """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm."""
@@ -909,7 +1006,10 @@ class StepEngine:
 
     def adam(self, fp: FlatParams, lr):
         hp = self.hyper
-        self._side_join()
+        if fp is self.fpG:
+            self._side_join("G")   # only G's pending side work (D's may still be running)
+        else:
+            self._side_join()
         fp.step += 1
         n = fp.n_live
         self.ops.adam(fp.flat[:n], fp.grad[:n], fp.m[:n], fp.v[:n], lr=lr, beta1=hp.beta1,
