@@ -350,6 +350,24 @@ def main():
     model.flush()
     host_ms = (time.perf_counter() - h0) * 1e3 / 2
     torch.cuda.synchronize()
+    # one more instrumented step (untimed) with every launch on one stream: the timed
+    # region overlaps weight gradients (side stream) with the input-gradient chain, so its
+    # per-launch durations include the other stream's contention; this gives each kernel
+    # family's rate in isolation (roofline.isolated)
+    ksum_iso = {}
+    if timer:
+        from pggan_amd import engine as _E
+        saved = (timer.rec, timer.shapes)
+        timer.rec, timer.shapes = {k: [] for k in timer.rec}, []
+        _E.FORCE_SERIAL = True
+        timer.on = True
+        step()
+        model.flush()
+        torch.cuda.synchronize()
+        timer.on = False
+        _E.FORCE_SERIAL = False
+        ksum_iso = timer.summary()
+        timer.rec, timer.shapes = saved
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -401,6 +419,20 @@ def main():
                                         launches_per_step=v["launches"])
                                 for k, v in sorted(ksum.items())},
                         per_resolution=timer.per_resolution())
+            if ksum_iso:
+                # the same groups from the isolated step (no overlap): achieved / frac per
+                # group against its own peak
+                def _iso(k, v):
+                    hbm = v["bound"] == "hbm"
+                    a = v["gbps"] if hbm else v["tflops"]
+                    pk = PEAK_HBM_GBS if hbm else PEAK_TFLOPS[timer.peak_key(k.split("/")[0])]
+                    return dict(achieved=round(a, 2), unit="GB/s" if hbm else "TFLOP/s",
+                                frac=round(a / pk, 4), avg_launch_us=round(v["avg_us"], 2),
+                                total_ms_per_step=round(v["total_ms"], 3))
+                roof["isolated"] = dict(
+                    note="one extra untimed step with every launch on one stream (per-launch "
+                         "durations without the side stream's overlap)",
+                    groups={k: _iso(k, v) for k, v in sorted(ksum_iso.items())})
         cpu = None
         log(f"timed: {1e3 * dt / args.steps:.3f} ms/step")
         if args.cpu_baseline == "auto" and world == 1:

@@ -265,6 +265,20 @@ int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream)
 /* dtype conversion helpers */
 int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void* stream);
 
+/* ---- training-image augmentation (SURVEY §8(f) GPU input pipeline): the transform chain
+ * of lib/dataset.py:106-117 after Resize -- RandomHorizontalFlip(0.5), ColorJitter(0.2, 0.2,
+ * 0.2, 0.01) in torchvision's random op order, ToTensor, Normalize(0.5, 0.5) -- on a batch of
+ * decoded, resized images: src uint8 [B][H][W][3] (4-byte aligned), dst fp32 [B][3][H][W]
+ * (16-byte aligned), params fp32 [B][12] = {flip (0/1), brightness, contrast, saturation,
+ * hue factor, fn_idx[0..3] (0 brightness, 1 contrast, 2 saturation, 3 hue), 1 - contrast,
+ * 1 - saturation, 0}.
+ * Jitter arithmetic: torchvision's tensor formulation (functional_tensor _blend /
+ * rgb_to_grayscale / _rgb2hsv / _hsv2rgb) in fp32.  W % 4 == 0.  The caller provides
+ * pg_augment_workspace_bytes(B, H, W) of device workspace. */
+size_t pg_augment_workspace_bytes(int B, int H, int W);
+int pg_augment_u8(int B, int H, int W, const void* src, const float* params, float* ws,
+                  size_t ws_bytes, float* dst, void* stream);
+
 /* ---- step plan: the kernel path of every 3x3 conv pass (forward, input
  * gradient, weight gradient) of one train_step at (stage, batch, dtype) -- the layer list of
  * pggan/nets.py:53-119 (G) and :164-239 (D) at scale_index = stage -- and the split-reduction

@@ -103,6 +103,8 @@ _SIGS = {
     "pg_adam": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _F, _I, _VP], _I),
     "pg_randn": ([_SZ, _U64, _U64, _VP, _VP], _I),
     "pg_cast": ([_I, _I, _SZ, _VP, _VP, _VP], _I),
+    "pg_augment_workspace_bytes": ([_I, _I, _I], _SZ),
+    "pg_augment_u8": ([_I, _I, _I, _VP, _VP, _VP, _SZ, _VP, _VP], _I),
     "pg_step_plan_create": ([_I, _I, ctypes.POINTER(ctypes.c_int), _I, _I,
                              ctypes.POINTER(ctypes.c_void_p)], _I),
     "pg_step_plan_workspace_size": ([_VP], _SZ),
@@ -437,6 +439,18 @@ class HipOps:
     def randn(self, out, seed, offset):
         self._cuda(out)
         self._chk(self.lib.pg_randn(out.numel(), seed, offset, _p(out), self._s()), "randn")
+
+    def augment_u8(self, src, params, dst, ws=None):
+        """src uint8 [B,H,W,3], params fp32 [B,12] (include/pggan_hip.h), dst fp32
+        [B,3,H,W]: flip + ColorJitter + ToTensor + Normalize (lib/dataset.py:106-117)."""
+        self._cuda(src, params, dst)
+        B, H, W, _ = src.shape
+        need = self.lib.pg_augment_workspace_bytes(B, H, W)
+        if ws is None or ws.numel() * 4 < need:
+            ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=src.device)
+        self._chk(self.lib.pg_augment_u8(B, H, W, _p(src), _p(params), _p(ws), ws.numel() * 4,
+                                         _p(dst), self._s()), "augment_u8")
+        return ws
 
     def cast(self, x, y):
         self._cuda(x, y)

@@ -1,0 +1,117 @@
+"""Training-image input pipeline: UnsupervisedDataset (lib/dataset.py:86-127)
+with the per-image augmentation on the GPU.
+
+Host: glob the roots like the reference (`*.*g` at every depth), decode + Resize with PIL
+(torchvision's Resize on a PIL image is PIL's bilinear resize, so this step is the
+reference's own code path) in a thread pool that prefetches the next batch while the
+current step runs; the uint8 HWC batch goes to HBM from pinned memory.
+
+GPU (`pg_augment_u8`, pggan_amd/csrc/augment.hip): RandomHorizontalFlip(0.5),
+ColorJitter(0.2, 0.2, 0.2, 0.01), ToTensor, Normalize(0.5, 0.5) in one pass over the
+batch (three launches).  The random parameters are drawn on the host with a torch CPU
+generator in torchvision's call order per image -- `torch.rand(1) < p` for the flip, then
+ColorJitter.get_params: `torch.randperm(4)`, brightness, contrast, saturation, hue
+`torch.empty(1).uniform_(lo, hi)` -- so a generator in the same state draws the same
+parameters as the reference's transform.  The jitter arithmetic is torchvision's tensor
+formulation in fp32; the reference applies the same four ops to the PIL image (uint8
+rounding after each op), which differs by a few /255 per pixel (tests/test_augment.py
+measures it against a PIL-path restatement).
+"""
+from __future__ import annotations
+
+import glob
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+# ColorJitter(0.2, 0.2, 0.2, 0.01) ranges (lib/dataset.py:110), flip probability (:108)
+JITTER = dict(brightness=(0.8, 1.2), contrast=(0.8, 1.2), saturation=(0.8, 1.2), hue=(-0.01, 0.01))
+FLIP_P = 0.5
+PSTRIDE = 12   # floats per image in the pg_augment_u8 parameter table
+
+
+def image_paths(roots):
+    """lib/dataset.py:89-99: `*.*g` directly under each root and in every subdirectory."""
+    paths = []
+    for r in roots or []:
+        paths += glob.glob(f"{r}/*.*g")
+        for root, dirs, _ in os.walk(r):
+            for d in dirs:
+                paths += glob.glob(f"{root}/{d}/*.*g")
+    return paths
+
+
+def load_u8(path, size):
+    """Decode + Resize((size, size)) (lib/dataset.py:107) -> uint8 [size, size, 3]."""
+    from PIL import Image
+    im = Image.open(path).convert("RGB").resize((size, size), Image.BILINEAR)
+    return np.asarray(im, dtype=np.uint8)
+
+
+def draw_params(B, gen):
+    """Per-image flip / ColorJitter parameters in torchvision's draw order -> fp32 [B, 12]:
+    {flip, brightness, contrast, saturation, hue, fn_idx[4], 1 - contrast, 1 - saturation, 0}
+    (1 - factor computed in double, as torchvision's _blend does)."""
+    p = np.zeros((B, PSTRIDE), np.float32)
+    for b in range(B):
+        flip = bool(torch.rand(1, generator=gen) < FLIP_P)
+        fn_idx = torch.randperm(4, generator=gen)
+        f = [float(torch.empty(1).uniform_(*JITTER[k], generator=gen))
+             for k in ("brightness", "contrast", "saturation", "hue")]
+        p[b, 0] = 1.0 if flip else 0.0
+        p[b, 1:5] = f
+        p[b, 5:9] = fn_idx.numpy()
+        p[b, 9] = 1.0 - f[1]
+        p[b, 10] = 1.0 - f[2]
+    return p
+
+
+class ImageFolderDataset:
+    """The image list of UnsupervisedDataset; `load(i)` decodes + resizes one image."""
+
+    def __init__(self, roots, scale_index=0):
+        self.paths = image_paths(roots)
+        self.size = 2 ** (scale_index + 2)
+
+    def __len__(self):
+        return len(self.paths)
+
+    def load(self, i):
+        return load_u8(self.paths[i], self.size)
+
+
+class BatchLoader:
+    """Decode/resize in `workers` host threads (PIL releases the GIL), one batch ahead;
+    flip + jitter + normalize on the GPU.  `next(indices, prefetch=None)` returns the fp32
+    NCHW [-1, 1] batch on `device` and starts decoding `prefetch` (the next indices)."""
+
+    def __init__(self, dataset, device, ops, seed=0, workers=None):
+        self.ds, self.dev, self.ops = dataset, torch.device(device), ops
+        if not hasattr(ops, "augment_u8"):
+            raise RuntimeError("pggan_amd: the input pipeline needs the HIP library (augment_u8)")
+        self.pool = ThreadPoolExecutor(max_workers=workers or min(16, os.cpu_count() or 1))
+        self.gen = torch.Generator().manual_seed(seed)
+        self._pending = None     # (indices, futures)
+        self._ws = None
+
+    def _submit(self, idx):
+        return tuple(idx), [self.pool.submit(self.ds.load, int(i)) for i in idx]
+
+    def next(self, idx, prefetch=None):
+        idx = tuple(int(i) for i in idx)
+        if self._pending is None or self._pending[0] != idx:
+            self._pending = self._submit(idx)
+        imgs = [f.result() for f in self._pending[1]]
+        self._pending = self._submit(prefetch) if prefetch is not None else None
+        B, S = len(imgs), self.ds.size
+        host = torch.from_numpy(np.stack(imgs)).pin_memory()
+        src = host.to(self.dev, non_blocking=True)
+        params = torch.from_numpy(draw_params(B, self.gen)).to(self.dev, non_blocking=True)
+        out = torch.empty(B, 3, S, S, dtype=torch.float32, device=self.dev)
+        self._ws = self.ops.augment_u8(src, params, out, ws=self._ws)
+        return out
+
+    def close(self):
+        self.pool.shutdown(wait=False)

@@ -161,6 +161,11 @@ class Hyper:
     W_drift: float = 0.0        # W_drift_D (wgan-gp mode only, pggan/loss.py:94-100)
 
 
+# measurement only (bench.py's isolated instrumented step): run the side-stream launches
+# inline on the current stream so per-launch HIP event durations exclude overlap
+FORCE_SERIAL = False
+
+
 class StepEngine:
     """All device buffers and kernel schedules for one (stage, batch, dtype)."""
 
@@ -439,7 +444,7 @@ class StepEngine:
         gscale * up2(g) * lrelu'(gzbits) (never materialised)."""
         c = self.packs[(net, key)][3]
         kw = dict(gzbits=gzbits, slope=SLOPE) if gzbits is not None else {}
-        if self.side is None:
+        if self.side is None or FORCE_SERIAL:
             need = self._ws_need("w", H, cin, cout, ups)
             self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
                                 scale=c * gscale, db=db, ws=self.ws if need else None, **kw)
@@ -457,7 +462,7 @@ class StepEngine:
         """Run a weight-gradient launch `fn` on the side stream (or inline without one).
         nets: whose buffers it reads (joins before those are overwritten).  Its inputs were
         written on the main stream, so the side stream first waits for it."""
-        if self.side is None:
+        if self.side is None or FORCE_SERIAL:
             return fn(*a, **kw)
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):

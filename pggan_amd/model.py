@@ -17,7 +17,6 @@ Differences (deliberate):
 """
 from __future__ import annotations
 
-import glob
 import math
 import os
 
@@ -27,6 +26,7 @@ import torch.distributed as dist
 
 from . import engine as E
 from .config import cfg_get
+from .data import BatchLoader, ImageFolderDataset
 from .loss import WGANGPLoss
 from .nets import Discriminator, Generator
 
@@ -71,33 +71,6 @@ class FlatAdam:
         if sd.get("param_groups"):
             g = sd["param_groups"][0]
             self.lr, self.betas, self.eps = g["lr"], tuple(g["betas"]), g["eps"]
-
-
-class ImageFolderDataset:
-    """UnsupervisedDataset (lib/dataset.py:86-127) without torchvision: glob *.*g under
-    each root, resize to 2^(s+2), random horizontal flip, to [-1,1] NCHW fp32."""
-
-    def __init__(self, roots, scale_index=0, seed=0):
-        self.paths = []
-        for r in roots or []:
-            self.paths += glob.glob(f"{r}/*.*g")
-            for root, dirs, _ in os.walk(r):
-                for d in dirs:
-                    self.paths += glob.glob(f"{root}/{d}/*.*g")
-        self.size = 2 ** (scale_index + 2)
-        self.rng = np.random.default_rng(seed)
-
-    def __len__(self):
-        return len(self.paths)
-
-    def __getitem__(self, i):
-        from PIL import Image
-        im = Image.open(self.paths[i]).convert("RGB").resize((self.size, self.size),
-                                                              Image.BILINEAR)
-        a = np.asarray(im, np.float32) / 127.5 - 1.0
-        if self.rng.random() < 0.5:
-            a = a[:, ::-1]
-        return torch.from_numpy(np.ascontiguousarray(a.transpose(2, 0, 1)))
 
 
 class ProgressiveGAN:
@@ -215,7 +188,7 @@ class ProgressiveGAN:
         missing = [r for r in roots if not os.path.isdir(r)]
         if missing:
             raise FileNotFoundError(f"dataset_root_list: no such directory: {missing}")
-        ds = ImageFolderDataset(roots, self.scale_index, seed=self.rank)
+        ds = ImageFolderDataset(roots, self.scale_index)
         if len(ds) == 0:
             raise RuntimeError(f"no images found under dataset_root_list {roots} (set "
                                f"synthetic_data: True to train on a synthetic batch)")
@@ -239,9 +212,16 @@ class ProgressiveGAN:
         B = self.args.batch_per_gpu
         if self._pos + B > len(self._order):
             self._pos = 0
-        items = [self.train_dataset[int(i)] for i in self._order[self._pos:self._pos + B]]
+        idx = self._order[self._pos:self._pos + B]
         self._pos += B
-        return torch.stack(items).to(self.device, non_blocking=True)
+        nxt = self._pos if self._pos + B <= len(self._order) else 0
+        if getattr(self, "_loader", None) is None or self._loader.ds is not self.train_dataset:
+            # decode + resize on host threads, flip + ColorJitter + normalize on the GPU
+            # (pggan_amd.data; lib/dataset.py:106-117)
+            from . import _lib
+            self._loader = BatchLoader(self.train_dataset, self.device, _lib.HipOps(torch.float32),
+                                       seed=1000 + self.rank)
+        return self._loader.next(idx, prefetch=self._order[nxt:nxt + B])
 
     def set_loss_collector(self):
         self._loss_collector = WGANGPLoss(self.args)
