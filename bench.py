@@ -367,6 +367,9 @@ def main():
         timer.on = False
         _E.FORCE_SERIAL = False
         ksum_iso = timer.summary()
+        if os.environ.get("PG_BENCH_SHAPES"):
+            with open(os.environ["PG_BENCH_SHAPES"] + ".iso.json", "w") as f:
+                json.dump(timer.per_shape(1), f, indent=1)
         timer.rec, timer.shapes = saved
     t = torch.tensor([dt], device=dev, dtype=torch.float64)
     if world > 1:
