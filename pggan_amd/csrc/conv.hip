@@ -1193,8 +1193,11 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // the pixels up to ~1024 workgroups, keeping >= 2 tiles per split
   // wide (MO = 4) tiles run one workgroup per CU with 4 tiles of loads in flight: one
   // wave of workgroups; the HBM-bound narrow ones use ~4 per CU
-  int target = pl.MO >= 4 ? 256 : 1024;
+  // (tools/wg_target_sweep.sh: 512 for the narrow tiles, 80.9 -> 59.2 us at 512^2 32->32,
+  // 86 -> 79 at 1024^2 16->16, 108 -> 99 at 1024^2 16->32: half the slab traffic)
+  int target = pl.MO >= 4 ? 256 : 512;
   if (const char* e = getenv("PG_WG_TARGET")) target = atoi(e);   // tuning runs only
+  if (const char* e = getenv("PG_WG_TARGET_NARROW")) { if (pl.MO < 4) target = atoi(e); }   // A/B
   int splits = base >= 256 ? 1 : pg_cdiv(target, base);
   const int max_splits = pl.ntiles / 2 > 1 ? pl.ntiles / 2 : 1;
   if (splits > max_splits) splits = max_splits;
