@@ -33,15 +33,25 @@ def run(ops, spec, B, iters):
         wpk = torch.randn(ops.packed_elems(0, cout, cin), device=dev, generator=g).to(bf) * 0.05
         Ho = H // 2 if fl & 16 else H
         y = torch.empty(B, Ho, Ho, cinp(cout), device=dev, dtype=bf)
-        aux = torch.randn(B, H, H, r8(cout), device=dev, generator=g).to(bf) if fl & 8 else None
+        aux = torch.randn(B, H, H, r8(cout), device=dev, generator=g).to(bf) if fl & (8 | 2048) else None
+        u8 = lambda C: torch.randint(0, 256, (B, H, H, (C + 7) // 8), device=dev, generator=g,
+                                     dtype=torch.uint8)
+        if fl & 256:                       # AUX_BITS: the mask operand is sign bits
+            aux = u8(cout)
+        xbits = u8(cp) if fl & 512 else None
+        y2 = None
+        if fl & 128:                       # Y2_BITS (with POOL): pre-pool sign bits
+            y2 = u8(cout)
+        elif fl & (64 | 2048):             # PIXNORM (keep) / PNBWD: the per-pixel factor
+            y2 = torch.rand(B, H, H, 1, device=dev, generator=g) + 0.5
         bias = torch.zeros(cout, device=dev) if fl & 2 else None
         nb = ops.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
         ws = torch.empty(max(nb // 4, 1), device=dev) if nb else None
 
         def f():
             ops.conv3x3(x, wpk, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=fl, bias=bias,
-                        aux=aux, ws=ws, out_scale=0.25 if fl & 16 else 1.0)
-        byts = x.numel() * 2 + y.numel() * 2 + (aux.numel() * 2 if aux is not None else 0)
+                        aux=aux, ws=ws, out_scale=0.25 if fl & 16 else 1.0, y2=y2, xbits=xbits)
+        byts = sum(t.numel() * t.element_size() for t in (x, y, aux, y2, xbits) if t is not None)
     else:
         Hin = H // 2 if fl else H
         x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
