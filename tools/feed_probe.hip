@@ -16,9 +16,11 @@ constexpr size_t WIN = 2u << 20;
 // piece: contiguous bytes per lane group (1024 = one contiguous KiB per wave load; 64 = the
 // conv tiles' halo pattern, 64 B of every `stride` bytes); win: the span the addresses wrap
 // in (2 MiB: L2-resident; 512 MiB: beyond the MALL, every pass from HBM)
+// (piece, stride, win: powers of two, so the address math is shifts and masks and the
+// probe measures the memory path, not a 64-bit division per load)
 __device__ __forceinline__ size_t paddr(size_t logical, int piece, int stride, size_t win) {
-  const size_t pc = logical / piece, in = logical - pc * piece;
-  return (pc * stride + in) % win;
+  const int lp = __builtin_ctz(piece), ls = __builtin_ctz(stride);
+  return (((logical >> lp) << ls) | (logical & (size_t)(piece - 1))) & (win - 1);
 }
 template <int NW, int DEPTH, bool DMA>
 __global__ __launch_bounds__(NW * 64) void feed(const char* __restrict__ src, int rounds,
