@@ -62,7 +62,8 @@ __global__ __launch_bounds__(NW * 64) void feed(const char* __restrict__ src, in
 template <int NW, int DEPTH, bool DMA>
 void run(const char* src, unsigned* sink, int piece = 1024, int stride = 1024, size_t win = WIN) {
   // logical bytes per workgroup: 2 MiB, or its own disjoint span of the HBM window
-  const size_t lb = win > WIN ? (win / 256) * piece / stride : (2u << 20);
+  size_t lb = win > WIN ? (win / 256) * piece / stride : (2u << 20);
+  if (lb < (512u << 10)) lb = 512u << 10;   // small windows (MALL-resident): wrap
   const int ncu = 256, rounds = (int)(lb / (NW * DEPTH * 1024));
   const int lds = DMA ? NW * DEPTH * 1024 : 0;
   CK(hipFuncSetAttribute((const void*)feed<NW, DEPTH, DMA>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -77,8 +78,8 @@ void run(const char* src, unsigned* sink, int piece = 1024, int stride = 1024, s
   CK(hipEventSynchronize(b));
   float ms = 0; CK(hipEventElapsedTime(&ms, a, b));
   const double bytes = (double)reps * ncu * rounds * NW * DEPTH * 1024.0;
-  printf("piece %4d stride %4d win %4zu MiB  %-4s waves %2d  KiB in flight/wave %2d  (/CU %3d)  %7.1f GB/s per CU  %6.2f TB/s total  %.1f us/launch\n",
-         piece, stride, win >> 20, DMA ? "dma" : "reg", NW, DEPTH, NW * DEPTH, bytes / (ms * 1e-3) / ncu / 1e9, bytes / (ms * 1e-3) / 1e12,
+  printf("piece %4d stride %4d win %4zu MiB rounds %3d  %-4s waves %2d  KiB in flight/wave %2d  (/CU %3d)  %7.1f GB/s per CU  %6.2f TB/s total  %.1f us/launch\n",
+         piece, stride, win >> 20, rounds, DMA ? "dma" : "reg", NW, DEPTH, NW * DEPTH, bytes / (ms * 1e-3) / ncu / 1e9, bytes / (ms * 1e-3) / 1e12,
          ms * 1e3 / reps);
 }
 
@@ -99,6 +100,12 @@ int main() {
     run<8, 8, true>(src, sink, 64, st);  run<8, 8, false>(src, sink, 64, st);
     run<4, 16, true>(src, sink, 64, st);
   }
+  // MALL-resident (32 MiB, past the 4 MiB L2 of an XCD, inside the 256 MiB MALL): what the
+  // 32^2-256^2 activations (4-34 MB at B = 4) are when the next conv reads them
+  const size_t MID = 32u << 20;
+  run<8, 8, true>(src, sink, 1024, 1024, MID);  run<8, 8, false>(src, sink, 1024, 1024, MID);
+  run<8, 8, true>(src, sink, 64, 256, MID);     run<8, 8, false>(src, sink, 64, 256, MID);
+  run<8, 16, true>(src, sink, 64, 256, MID);    run<8, 16, true>(src, sink, 1024, 1024, MID);
   run<8, 8, true>(src, sink, 1024, 1024, BIG);  run<8, 8, false>(src, sink, 1024, 1024, BIG);
   run<8, 8, true>(src, sink, 64, 256, BIG);     run<8, 8, false>(src, sink, 64, 256, BIG);
   run<8, 16, true>(src, sink, 64, 256, BIG);
