@@ -87,12 +87,14 @@ class BatchLoader:
     flip + jitter + normalize on the GPU.  `next(indices, prefetch=None)` returns the fp32
     NCHW [-1, 1] batch on `device` and starts decoding `prefetch` (the next indices)."""
 
-    def __init__(self, dataset, device, ops, seed=0, workers=None):
+    def __init__(self, dataset, device, ops, seed=0, workers=None, gen=None):
+        """gen: the torch CPU generator the augmentation parameters are drawn from (shared
+        across the loaders of successive stages); default a new one seeded with `seed`."""
         self.ds, self.dev, self.ops = dataset, torch.device(device), ops
         if not hasattr(ops, "augment_u8"):
             raise RuntimeError("pggan_amd: the input pipeline needs the HIP library (augment_u8)")
         self.pool = ThreadPoolExecutor(max_workers=workers or min(16, os.cpu_count() or 1))
-        self.gen = torch.Generator().manual_seed(seed)
+        self.gen = gen if gen is not None else torch.Generator().manual_seed(seed)
         self._pending = None     # (indices, futures)
         self._ws = None
 
@@ -114,4 +116,6 @@ class BatchLoader:
         return out
 
     def close(self):
-        self.pool.shutdown(wait=False)
+        """Stop the decode threads; pending prefetches are cancelled."""
+        self._pending = None
+        self.pool.shutdown(wait=False, cancel_futures=True)

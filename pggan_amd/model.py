@@ -198,12 +198,12 @@ class ProgressiveGAN:
         self.train_dataset = ds
 
     def set_data_iterator(self):
-        """lib/model.py:44-52: per-rank shard of a shuffled index order (DistributedSampler)."""
+        """lib/model.py:44-52: one process reads the dataset in order (DataLoader without a
+        sampler, no shuffle); with DP each rank reads its DistributedSampler shard (seed 0,
+        set_epoch never called, so every epoch repeats the same order: SURVEY Appendix A.4)."""
         self._order, self._pos = None, 0
         if self.train_dataset is not None:
-            n = len(self.train_dataset)
-            idx = np.arange(n)[self.rank::self.world]
-            self._order = idx
+            self._order = sampler_order(len(self.train_dataset), self.rank, self.world)
 
     def load_next_batch(self):
         """pggan/model.py:104-115."""
@@ -217,10 +217,17 @@ class ProgressiveGAN:
         nxt = self._pos if self._pos + B <= len(self._order) else 0
         if getattr(self, "_loader", None) is None or self._loader.ds is not self.train_dataset:
             # decode + resize on host threads, flip + ColorJitter + normalize on the GPU
-            # (pggan_amd.data; lib/dataset.py:106-117)
+            # (pggan_amd.data; lib/dataset.py:106-117).  A new stage's loader replaces the
+            # previous one (its threads and pending decodes are cancelled) and keeps drawing
+            # augmentation parameters from the same generator, so stages do not replay one
+            # parameter sequence.
             from . import _lib
+            if getattr(self, "_loader", None) is not None:
+                self._loader.close()
+            if getattr(self, "_aug_gen", None) is None:
+                self._aug_gen = torch.Generator().manual_seed(1000 + self.rank)
             self._loader = BatchLoader(self.train_dataset, self.device, _lib.HipOps(torch.float32),
-                                       seed=1000 + self.rank)
+                                       gen=self._aug_gen)
         return self._loader.next(idx, prefetch=self._order[nxt:nxt + B])
 
     def set_loss_collector(self):
@@ -276,6 +283,15 @@ class ProgressiveGAN:
         img_real = self.load_next_batch()
         B = img_real.shape[0]
         eng = self._engine(B)
+        # in-place edits of G / D parameters outside the engine (load_state_dict, p.copy_,
+        # EMA copies) bump the parameters' version counters: repack the weights before the
+        # step uses them.  Edits through `p.data` bypass the counters; call _params_changed()
+        # after those.
+        ver = (sum(p._version for p in self.G.parameters()),
+               sum(p._version for p in self.D.parameters()))
+        if ver != getattr(self, "_param_ver", ver):
+            self._params_changed()
+        self._param_ver = ver
         self.hyper.lr_G, self.hyper.lr_D = self.opt_G.lr, self.opt_D.lr
         z = getattr(self, "_z", None)
         if z is None or z.shape[1] != B:
@@ -400,14 +416,62 @@ class ProgressiveGAN:
         self._params_changed()
 
     def save_image(self, images, step):
-        """lib/utils.py:86-103: grid of up to 8 images per row, rows = tensors, [-1,1] ->
-        [0,255], written to {save_root}/{run_id}/imgs/e{step}.jpg."""
+        """lib/utils.py:86-91: make_grid_image(images) * 255 written to
+        {save_root}/{run_id}/imgs/e{step}.jpg (cv2.imwrite saturates and rounds to uint8)."""
         from PIL import Image
-        rows = []
-        for t in images:
-            t = t[:8].detach().float().cpu().clamp(-1, 1) * 0.5 + 0.5
-            rows.append(torch.cat(list(t), dim=2))
-        grid = torch.cat(rows, dim=1).permute(1, 2, 0).numpy()
+        grid = make_grid_image(images).permute(1, 2, 0).numpy().astype(np.float64) * 255
         d = f"{self.args.save_root}/{self.args.run_id}/imgs"
         os.makedirs(d, exist_ok=True)
-        Image.fromarray((grid * 255).astype(np.uint8)).save(f"{d}/e{step}.jpg")
+        Image.fromarray(np.clip(np.rint(grid), 0, 255).astype(np.uint8)).save(f"{d}/e{step}.jpg")
+
+
+def sampler_order(n, rank, world):
+    """The sample order rank `rank` of `world` reads (lib/model.py:50-51).  world == 1: the
+    reference builds its DataLoader without a sampler, i.e. in order.  world > 1:
+    torch.utils.data.DistributedSampler(dataset) with its defaults (shuffle, seed 0,
+    drop_last False) at epoch 0 -- torch.randperm(n) from a generator seeded with 0, padded
+    by wrapping to a multiple of world, then every world-th index from rank."""
+    if world <= 1:
+        return np.arange(n)
+    g = torch.Generator().manual_seed(0)
+    idx = torch.randperm(n, generator=g).tolist()
+    total = math.ceil(n / world) * world
+    pad = total - n
+    if pad <= n:
+        idx += idx[:pad]
+    else:
+        idx += (idx * math.ceil(pad / n))[:pad]
+    return np.asarray(idx[rank:total:world], dtype=np.int64)
+
+
+def make_grid_image(list_of_tensors):
+    """lib/utils.py:94-103: one torchvision.utils.make_grid row per tensor (its first 8
+    images, nrow = their count, padding 2, pad value 0), each row * 0.5 + 0.5, rows stacked
+    along the height.  Returns a CPU fp32 [C, H, W] tensor (the padding ends up 0.5, values
+    are not clamped, as in the reference)."""
+    rows = []
+    for t in list_of_tensors:
+        t = t[:8].detach().float().cpu()
+        rows.append(_make_grid(t, nrow=t.shape[0]) * 0.5 + 0.5)
+    return torch.cat(rows, dim=1)
+
+
+def _make_grid(t, nrow, padding=2, pad_value=0.0):
+    """torchvision.utils.make_grid's layout for a [N, C, H, W] batch (normalize=False)."""
+    if t.dim() == 4 and t.shape[1] == 1:
+        t = torch.cat((t, t, t), 1)
+    if t.shape[0] == 1:
+        return t.squeeze(0)
+    n = t.shape[0]
+    xmaps = min(nrow, n)
+    ymaps = int(math.ceil(float(n) / xmaps))
+    h, w = t.shape[2] + padding, t.shape[3] + padding
+    grid = t.new_full((t.shape[1], h * ymaps + padding, w * xmaps + padding), pad_value)
+    k = 0
+    for y in range(ymaps):
+        for x in range(xmaps):
+            if k >= n:
+                break
+            grid[:, y * h + padding:(y + 1) * h, x * w + padding:(x + 1) * w] = t[k]
+            k += 1
+    return grid
