@@ -319,20 +319,34 @@ def main():
 
     log = lambda m: print(f"[bench] {m}", file=sys.stderr, flush=True)
     log(f"stage {s} batch {B} world {world}: {args.warmup} warm-up steps")
+    # one process: from the second step on, train_step replays the step captured as a
+    # hipGraph (ProgressiveGAN.use_graph; PG_GRAPH=0 keeps it eager)
     for _ in range(args.warmup):
         step()
     model.flush()
     torch.cuda.synchronize()
+    # host-side cost of enqueueing one step (kernels are not waited for): if this is close
+    # to ms_per_step the step is launch-bound, not GPU-bound.  Measured on the steps the
+    # timed loop runs (graph replays in one process), before it.
+    h0 = time.perf_counter()
+    for _ in range(2):
+        step()
+    model.flush()
+    host_ms = (time.perf_counter() - h0) * 1e3 / 2
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    replays0 = model.graph_replays
     t0 = time.perf_counter()
     for i in range(args.steps):
         # per-launch HIP events on the conv kernels during the last timed step only: each
         # event pair costs ~7 us of GPU time, so instrumenting every step would cost ~10 %
-        # of the throughput being measured
-        if timer:
-            timer.on = i == args.steps - 1
+        # of the throughput being measured.  That step runs eagerly (events around each
+        # launch), the others are graph replays.
+        if timer and i == args.steps - 1:
+            timer.on = True
+            model.use_graph = False
         step()
     model.flush()        # the last step's (deferred) generator update is part of the step
     torch.cuda.synchronize()
@@ -341,15 +355,7 @@ def main():
     dt = time.perf_counter() - t0
     if timer:
         timer.on = False
-    # host-side cost of enqueueing one step (kernels are not waited for): if this is close
-    # to ms_per_step the step is launch-bound, not GPU-bound
-    torch.cuda.synchronize()
-    h0 = time.perf_counter()
-    for _ in range(2):
-        step()
-    model.flush()
-    host_ms = (time.perf_counter() - h0) * 1e3 / 2
-    torch.cuda.synchronize()
+    graph_steps = model.graph_replays - replays0
     # one more instrumented step (untimed) with every launch on one stream: the timed
     # region overlaps weight gradients (side stream) with the input-gradient chain, so its
     # per-launch durations include the other stream's contention; this gives each kernel
@@ -467,6 +473,7 @@ def main():
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
             "host_enqueue_ms_per_step": round(host_ms, 3),
+            "graph_replayed_steps": graph_steps,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

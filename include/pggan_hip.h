@@ -75,6 +75,9 @@ int pg_version(void);
  * dtype, aux_cs), y2 = r (fp32 [B*H*W], from the forward).  Not with BIAS / POOL / MASK /
  * ACCUM / PIXNORM / bit flags. */
 #define PG_CONV_PNBWD 2048
+/* Channel-blocked activations: the operand is [B][C/32][H][W][32] (C = its channel stride,
+ * a multiple of 32) instead of NHWC -- a 32-channel slice of a pixel row is contiguous. */
+#define PG_CONV_X_BLK 4096
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -260,8 +263,20 @@ int pg_mul_add(size_t n, const float* x, const float* y, const float* z, float* 
 int pg_adam(size_t n, float* p, const float* g, float* m, float* v, float lr, float beta1,
             float beta2, float eps, int step, void* stream);
 
+/* Adam with the step count in DEVICE memory, for a step captured once and replayed as a
+ * hipGraph: bumps *step, then updates with the bias corrections of the new count taken from
+ * `table` (DEVICE, tlen pairs {lr / (1 - beta1^t), sqrt(1 - beta2^t)} for t = 1..tlen, built
+ * by pg_adam_table on the host with pg_adam's double arithmetic; counts past tlen use the last
+ * pair, which pg_adam_table_len makes exact) -- the same update as pg_adam at that step. */
+int pg_adam_table_len(float lr, float beta1, float beta2);
+int pg_adam_table(float lr, float beta1, float beta2, int tlen, float* host_table);
+int pg_adam_dev(size_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+                float eps, const float* table, int tlen, int* step, void* stream);
+
 /* ---- N(0,1) latents (counter-based, deterministic in (seed, offset)) */
 int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream);
+/* the same draw with the offset in DEVICE memory; *offset then advances by n (graph replay) */
+int pg_randn_dev(size_t n, uint64_t seed, uint64_t* offset, float* out, void* stream);
 /* dtype conversion helpers */
 int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void* stream);
 

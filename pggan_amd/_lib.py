@@ -102,6 +102,10 @@ _SIGS = {
     "pg_mul_add": ([_SZ, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_adam": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _F, _I, _VP], _I),
     "pg_randn": ([_SZ, _U64, _U64, _VP, _VP], _I),
+    "pg_randn_dev": ([_SZ, _U64, _VP, _VP, _VP], _I),
+    "pg_adam_table_len": ([_F, _F, _F], _I),
+    "pg_adam_table": ([_F, _F, _F, _I, _VP], _I),
+    "pg_adam_dev": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _VP, _I, _VP, _VP], _I),
     "pg_cast": ([_I, _I, _SZ, _VP, _VP, _VP], _I),
     "pg_augment_workspace_bytes": ([_I, _I, _I], _SZ),
     "pg_augment_u8": ([_I, _I, _I, _VP, _VP, _VP, _SZ, _VP, _VP], _I),
@@ -435,6 +439,31 @@ class HipOps:
         self._cuda(p, g, m, v)
         self._chk(self.lib.pg_adam(p.numel(), _p(p), _p(g), _p(m), _p(v), lr, beta1, beta2, eps,
                                    step, self._s()), "adam")
+
+    def adam_table(self, lr, beta1, beta2, device):
+        """Device table of pg_adam_dev's bias corrections for (lr, beta1, beta2), cached."""
+        key = (float(lr), float(beta1), float(beta2), str(device))
+        tabs = self.__dict__.setdefault("_adam_tabs", {})
+        if key not in tabs:
+            n = int(self.lib.pg_adam_table_len(lr, beta1, beta2))
+            host = (ctypes.c_float * (2 * n))()
+            self._chk(self.lib.pg_adam_table(lr, beta1, beta2, n, host), "adam_table")
+            t = torch.frombuffer(bytearray(bytes(host)), dtype=torch.float32).to(device)
+            tabs[key] = (t, n)
+        return tabs[key]
+
+    def adam_dev(self, p, g, m, v, *, lr, beta1, beta2, eps, step_dev):
+        """Adam with the step count in device memory (bumped by the launch): replayable."""
+        self._cuda(p, g, m, v, step_dev)
+        tab, n = self.adam_table(lr, beta1, beta2, p.device)
+        self._chk(self.lib.pg_adam_dev(p.numel(), _p(p), _p(g), _p(m), _p(v), beta1, beta2, eps,
+                                       _p(tab), n, _p(step_dev), self._s()), "adam_dev")
+
+    def randn_dev(self, out, seed, offset_dev):
+        """pg_randn with the offset in device memory (advanced by out.numel())."""
+        self._cuda(out, offset_dev)
+        self._chk(self.lib.pg_randn_dev(out.numel(), seed, _p(offset_dev), _p(out), self._s()),
+                  "randn_dev")
 
     def randn(self, out, seed, offset):
         self._cuda(out)

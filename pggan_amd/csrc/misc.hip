@@ -1095,6 +1095,30 @@ __global__ void adam_kernel(size_t n, float* p, const float* g, float* m, float*
   }
 }
 
+// Adam with the step count in device memory (graph replay): `tick` bumps the counter, the
+// update reads its bias corrections from a host-built table indexed by the new count (the
+// last entry repeats once both corrections are exactly 1.0 in double), so every replay of a
+// captured step uses the step number it really is, with the host's arithmetic (pg_adam).
+__global__ void counter_tick_kernel(int* step) { *step += 1; }
+
+__global__ void adam_dev_kernel(size_t n, float* p, const float* g, float* m, float* v, float beta1,
+                                float beta2, float eps, const float* table, int tlen,
+                                const int* step) {
+  const int s = *step;
+  const int k = (s < tlen ? s : tlen) - 1;
+  const float step_size = table[2 * k], bc2_sqrt = table[2 * k + 1];
+  GRID_STRIDE(i, n) {
+    const float gi = g[i];
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
 // ------------------------------------------------------------ RNG / cast
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9e3779b97f4a7c15ull;
@@ -1111,6 +1135,18 @@ __global__ void randn_kernel(size_t n, uint64_t seed, uint64_t offset, float* ou
     out[i] = sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
   }
 }
+
+// offset read from device memory (graph replay); the counter is then advanced by n
+__global__ void randn_dev_kernel(size_t n, uint64_t seed, const uint64_t* offset, float* out) {
+  const uint64_t off = *offset;
+  GRID_STRIDE(i, n) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(off + i));
+    const float u1 = ((float)(uint32_t)(h >> 40) + 0.5f) * (1.f / 16777216.f);
+    const float u2 = ((float)(uint32_t)((h >> 16) & 0xffffffu)) * (1.f / 16777216.f);
+    out[i] = sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
+  }
+}
+__global__ void u64_add_kernel(uint64_t* c, uint64_t d) { *c += d; }
 
 template <typename A, typename B>
 __global__ void cast_kernel(size_t n, const A* x, B* y) {
@@ -1671,6 +1707,47 @@ int pg_adam(size_t n, float* p, const float* g, float* m, float* v, float lr, fl
   const float bc2_sqrt = (float)sqrt(bc2);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
                      v, beta1, beta2, eps, step_size, bc2_sqrt);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_adam_table_len(float lr, float beta1, float beta2) {
+  (void)lr;
+  int t = 1;
+  while (t < (1 << 20) && (1.0 - pow((double)beta1, (double)t) != 1.0 ||
+                           1.0 - pow((double)beta2, (double)t) != 1.0))
+    ++t;
+  return t;
+}
+
+int pg_adam_table(float lr, float beta1, float beta2, int tlen, float* host_table) {
+  PG_CHECK_ARG(host_table && tlen >= 1, "adam_table: bad args");
+  for (int k = 0; k < tlen; ++k) {   // exactly pg_adam's scalars for step k + 1
+    const double bc1 = 1.0 - pow((double)beta1, (double)(k + 1));
+    const double bc2 = 1.0 - pow((double)beta2, (double)(k + 1));
+    host_table[2 * k] = (float)(lr / bc1);
+    host_table[2 * k + 1] = (float)sqrt(bc2);
+  }
+  return PG_OK;
+}
+
+int pg_adam_dev(size_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+                float eps, const float* table, int tlen, int* step, void* stream) {
+  PG_CHECK_ARG(p && g && m && v && table && step && tlen >= 1, "adam_dev: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(counter_tick_kernel, dim3(1), dim3(1), 0, st, step);
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, p, g, m, v, beta1,
+                     beta2, eps, table, tlen, (const int*)step);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_randn_dev(size_t n, uint64_t seed, uint64_t* offset, float* out, void* stream) {
+  PG_CHECK_ARG(out && offset, "randn_dev: null pointer");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(randn_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, seed,
+                     (const uint64_t*)offset, out);
+  hipLaunchKernelGGL(u64_add_kernel, dim3(1), dim3(1), 0, st, offset, (uint64_t)n);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

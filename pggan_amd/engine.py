@@ -125,6 +125,10 @@ class FlatParams:
         self.m = torch.zeros_like(self.flat)
         self.v = torch.zeros_like(self.flat)
         self.step = 0
+        # the step count Adam reads on the device (pg_adam_dev: graph replay); _step_dev_host
+        # is the value it is known to hold (None: unknown, rewritten before the next update)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=device)
+        self._step_dev_host = 0
         self.shapes = shp
         self.dead = set(dead)
         self.views = {n: self._view(self.flat, n) for n in self.names}
@@ -1015,8 +1019,16 @@ class StepEngine:
             self._side_join("G")   # only G's pending side work (D's may still be running)
         else:
             self._side_join()
-        fp.step += 1
         n = fp.n_live
+        if hasattr(self.ops, "adam_dev"):
+            if fp._step_dev_host != fp.step:   # a reset / checkpoint load changed the count
+                fp.step_dev.fill_(fp.step)
+            fp.step += 1
+            fp._step_dev_host = fp.step
+            self.ops.adam_dev(fp.flat[:n], fp.grad[:n], fp.m[:n], fp.v[:n], lr=lr, beta1=hp.beta1,
+                              beta2=hp.beta2, eps=hp.eps, step_dev=fp.step_dev)
+            return
+        fp.step += 1
         self.ops.adam(fp.flat[:n], fp.grad[:n], fp.m[:n], fp.v[:n], lr=lr, beta1=hp.beta1,
                       beta2=hp.beta2, eps=hp.eps, step=fp.step)
 

@@ -278,6 +278,75 @@ class ProgressiveGAN:
         for eng in self._engines.values():
             eng.flush()
 
+    # one training step captured once per (stage, schedule scalars) and replayed as a
+    # hipGraph (world == 1): the host enqueue of ~600 launches becomes one graph launch.
+    # PG_GRAPH=0 keeps every step eager.
+    use_graph = os.environ.get("PG_GRAPH", "1") != "0"
+    graph_replays = 0
+
+    def _graph_key(self, eng, B):
+        """The key of a replayable step, or None when this step must run eagerly: one
+        process, the HIP op set (device-side step counters), no trace hook, packed weights,
+        no deferred generator update."""
+        if not (self.use_graph and self._exchange is None and self.device.type == "cuda" and
+                hasattr(eng.ops, "randn_dev") and hasattr(eng.ops, "adam_dev") and
+                eng.trace is None and eng.grad_ready is None and not E.FORCE_SERIAL and
+                eng._pending_G is None and all(eng._packed.values())):
+            return None
+        h = self.hyper
+        return (id(eng), id(self.fpG), id(self.fpD), B, float(self.G.alpha), float(self.D.alpha),
+                h.lr_G, h.lr_D, h.beta1, h.beta2, h.eps, h.W_adv, h.slope_cfg, h.gp_mode, h.W_gp,
+                h.W_drift)
+
+    def _step_body(self, eng, real, B):
+        """The work of one step after the batch is resident: latents, then the engine step."""
+        z = self._z
+        if hasattr(eng.ops, "randn_dev"):
+            off = getattr(self, "_rng_off", None)
+            if off is None or off.device != self.device:
+                off = self._rng_off = torch.zeros(1, dtype=torch.int64, device=self.device)
+                self._rng_off_host = None
+            if self._rng_off_host != self._rng_step * z.numel():   # keep host and device in step
+                off.fill_(self._rng_step * z.numel())
+            eng.ops.randn_dev(z, 1000 * self.rank + 17, off)
+            self._rng_off_host = (self._rng_step + 1) * z.numel()
+        else:
+            eng.ops.randn(z, 1000 * self.rank + 17, self._rng_step * z.numel())
+        self._rng_step += 1
+        gp_eps = None
+        if self.hyper.gp_mode != "r1":
+            gp_eps = torch.rand(B, 1, device=self.device)
+        return eng.train_step(real, z[0], z[1], float(self.G.alpha), float(self.D.alpha),
+                              grad_hook=self._grad_hook, gp_eps=gp_eps)
+
+    def _replay(self, eng, key, img_real, B):
+        """Run the step from the captured graph (capturing it on the second step with the
+        same key); returns the engine's outputs or None to run eagerly."""
+        gs = self.__dict__.setdefault("_gstate", {})
+        if gs.get("key") != key:
+            gs.clear()
+            gs["key"] = key          # first step with this key: eager (warms every lazy buffer)
+            return None
+        if "graph" not in gs:
+            gs["real"] = img_real if img_real is self.synthetic else img_real.clone()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                gs["out"] = self._step_body(eng, gs["real"], B)
+            gs["graph"] = g
+            # capture ran the host bookkeeping of one step (step counts, RNG offset) without
+            # the kernels; the replay below executes them
+        else:
+            if img_real is not gs["real"]:
+                gs["real"].copy_(img_real)
+            self._rng_step += 1
+            self._rng_off_host = self._rng_step * self._z.numel()
+            for fp in (self.fpG, self.fpD):
+                fp.step += 1
+                fp._step_dev_host = fp.step
+        gs["graph"].replay()
+        self.graph_replays += 1
+        return gs["out"]
+
     def train_step(self):
         """pggan/model.py:206-255; returns [img_real, img_fake]."""
         img_real = self.load_next_batch()
@@ -296,14 +365,13 @@ class ProgressiveGAN:
         z = getattr(self, "_z", None)
         if z is None or z.shape[1] != B:
             self._z = z = torch.empty(2, B, self.args.latent_dim, device=self.device)
-        eng.ops.randn(z, 1000 * self.rank + 17, self._rng_step * z.numel())
-        self._rng_step += 1
-        gp_eps = None
-        if self.hyper.gp_mode != "r1":
-            gp_eps = torch.rand(B, 1, device=self.device)
-        img_real, _, img_fake = eng.train_step(img_real, z[0], z[1], float(self.G.alpha),
-                                               float(self.D.alpha), grad_hook=self._grad_hook,
-                                               gp_eps=gp_eps)
+        key = self._graph_key(eng, B)
+        out = self._replay(eng, key, img_real, B) if key is not None else None
+        if out is None:
+            if key is None:        # an eager step may change what a captured graph assumed
+                self.__dict__.pop("_gstate", None)
+            out = self._step_body(eng, img_real, B)
+        img_real, _, img_fake = out
         self.loss_collector.attach(eng.loss, self.hyper.gp_mode)
         return [img_real, img_fake]
 

@@ -1,0 +1,79 @@
+"""The hipGraph-replayed training step (ProgressiveGAN.train_step with use_graph, world 1)
+against the same model stepped eagerly, after every step, including across a change of
+alpha (a new capture) and an external parameter edit (load_state_dict: repack + recapture):
+the latents bitwise equal (device-side RNG offset), the Adam step counts equal on host and
+device, and losses / gradients / parameters / moments equal up to the run-to-run spread of
+the kernels' fp32 atomics (to/fromRGB weight gradients, bias gradients, the R1 sum), which
+makes two eager runs differ in the last bits too: a replay of the wrong step (stale
+latents, a wrong bias correction -- 41 % between steps 1 and 2) fails by orders of
+magnitude."""
+import pytest
+import torch
+
+from gen_inputs import TINY_DEPTHS
+from test_model_api import make_args
+
+pytestmark = pytest.mark.gpu
+
+
+def build(args, graph, s):
+    from pggan_amd.model import ProgressiveGAN
+    ProgressiveGAN.ops_factory = None
+    torch.manual_seed(7)
+    m = ProgressiveGAN(args, 0)
+    m.use_graph = graph
+    m.initialize_models()
+    for i in range(1, s + 1):
+        m.G.add_block(args.depths[i])
+        m.D.add_block(args.depths[i])
+    m.scale_index = s
+    m.set_optimizers()
+    m.set_dataset()
+    m.set_data_iterator()
+    m.set_loss_collector()
+    return m
+
+
+def state(m):
+    out = {"loss": m._engines[next(iter(m._engines))].loss.clone(), "z": m._z.clone()}
+    for n, fp in (("G", m.fpG), ("D", m.fpD)):
+        out[n + "p"], out[n + "g"] = fp.flat.clone(), fp.grad.clone()
+        out[n + "m"], out[n + "v"] = fp.m.clone(), fp.v.clone()
+    return out
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_graph_replay_bitwise_equals_eager(tmp_path, dtype):
+    args = make_args(tmp_path, depths=list(TINY_DEPTHS), compute_dtype=dtype)
+    s = 3
+    eager, graph = build(args, False, s), build(args, True, s)
+    for m in (eager, graph):
+        m.G.alpha = m.D.alpha = 0.5
+    for step in range(9):
+        if step == 4:           # alpha ramp: the graph is recaptured for the new scalars
+            for m in (eager, graph):
+                m.G.alpha = m.D.alpha = 0.75
+        if step == 5:           # external edit: version counters bump -> repack, eager step
+            sd = {k: v.clone() * 1.01 for k, v in eager.G.state_dict().items()}
+            for m in (eager, graph):
+                m.G.load_state_dict(sd)
+        eager.train_step()
+        graph.train_step()
+        torch.cuda.synchronize()
+        a, b = state(eager), state(graph)
+        assert torch.equal(a["z"], b["z"]), step
+        for k in a:
+            d = float((a[k].double() - b[k].double()).norm())
+            n = float(a[k].double().norm())
+            # gradients and the moments built from them (beta1 = 0: m is the gradient) /
+            # everything else
+            tol = 1e-3 if k[-1] in "gmv" else 1e-5
+            assert d <= tol * max(n, 1e-30), (step, k, d / max(n, 1e-30))
+        # beta1 = 0: Adam's first update is ~lr * sign(g), so a last-bit difference of a
+        # near-zero gradient moves one parameter by up to ~2 lr
+        dp = float((a["Gp"] - b["Gp"]).abs().max())
+        assert dp <= 2 * (step + 1) * graph.hyper.lr_G, (step, dp)
+        assert eager.fpG.step == graph.fpG.step == step + 1
+        assert int(graph.fpD.step_dev.item()) == graph.fpD.step
+        if step in (2, 3, 8):   # steady state: a captured graph replayed
+            assert "graph" in graph._gstate, step
