@@ -287,9 +287,11 @@ int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void*
  * (16-byte aligned), params fp32 [B][12] = {flip (0/1), brightness, contrast, saturation,
  * hue factor, fn_idx[0..3] (0 brightness, 1 contrast, 2 saturation, 3 hue), 1 - contrast,
  * 1 - saturation, 0}.
- * Jitter arithmetic: torchvision's tensor formulation (functional_tensor _blend /
- * rgb_to_grayscale / _rgb2hsv / _hsv2rgb) in fp32.  W % 4 == 0.  The caller provides
- * pg_augment_workspace_bytes(B, H, W) of device workspace. */
+ * Jitter arithmetic: the reference's PIL path (torchvision functional_pil: ImageEnhance
+ * Brightness / Contrast / Color blends and the uint8 shift of PIL's HSV hue band) in Pillow's
+ * libImaging arithmetic, uint8 after every op: byte-identical to the reference transform.
+ * W % 4 == 0.  The caller provides pg_augment_workspace_bytes(B, H, W) of device workspace
+ * (16-byte aligned). */
 size_t pg_augment_workspace_bytes(int B, int H, int W);
 int pg_augment_u8(int B, int H, int W, const void* src, const float* params, float* ws,
                   size_t ws_bytes, float* dst, void* stream);

@@ -1,111 +1,43 @@
-"""TEST INFRASTRUCTURE ONLY (the checker, never the product path): CPU restatement of the
+"""TEST INFRASTRUCTURE ONLY (the checker, never the product path): CPU statements of the
 reference's training-image transform after the resize, lib/dataset.py:106-117
 
     RandomHorizontalFlip(p=0.5) -> ColorJitter(0.2, 0.2, 0.2, 0.01) -> ToTensor
     -> Normalize((0.5, 0.5, 0.5), (0.5, 0.5, 0.5)),
 
-in two forms:
+which the reference applies to a PIL image, so ColorJitter runs torchvision's PIL path
+(torchvision/transforms/functional_pil.py, torchvision 0.12 as pinned with torch 1.11):
+ImageEnhance.Brightness / Contrast / Color and adjust_hue (the H band of PIL's HSV mode
+shifted by np.uint8(hue_factor * 255), wrapping).
 
-* `augment_tensor`: torchvision's tensor formulation (torchvision/transforms/
-  functional_tensor.py: _blend, rgb_to_grayscale, adjust_brightness / contrast /
-  saturation / hue, _rgb2hsv, _hsv2rgb) in numpy float32 -- what pg_augment_u8 computes;
-* `augment_pil`: the reference's own path, the ops applied to the PIL image
-  (torchvision/transforms/functional_pil.py: ImageEnhance.Brightness / Contrast / Color,
-  hue through PIL's HSV mode with a uint8 shift of the H band), then ToTensor + Normalize.
+* `augment_pil`: that path itself -- the same PIL calls (PIL is installed here; torchvision
+  is not, so its four adjust_* wrappers are restated line for line).
+* `augment_pil_np`: a numpy restatement of the C arithmetic under those calls (Pillow's
+  libImaging: Blend.c ImagingBlend, Convert.c rgb2l / rgb2hsv_row / hsv2rgb, ImageStat's
+  mean), i.e. exactly what pg_augment_u8 computes.  Each piece is checked against PIL
+  exhaustively where the domain allows (every RGB colour for L and HSV, every HSV triple
+  for the way back, every byte pair for blend over many factors: tests/test_augment.py),
+  and the whole chain against `augment_pil` byte for byte.
 
-torchvision is not installed in this image (the reference's dataset module cannot be
-imported here), so neither form is checked against the reference's own run: the tensor
-form is a restatement of torchvision's published algorithm (parity unpinned against a
-torchvision run), and the PIL form calls the same PIL functions torchvision's PIL path calls.
 Parameters: per image {flip, brightness, contrast, saturation, hue, fn_idx[4]} as drawn by
-pggan_amd.data.draw_params (torchvision's ColorJitter.get_params order).
+pggan_amd.data.draw_params (torchvision's RandomHorizontalFlip + ColorJitter.get_params
+call order).  The hue shift np.uint8(hue_factor * 255) of a negative factor is taken as
+truncation toward zero, then wrapping (the x86 behaviour numpy had for that cast).
 """
 from __future__ import annotations
 
 import numpy as np
 
-F32 = np.float32
+F32, F64 = np.float32, np.float64
 
 
-def _gray(img):
-    # rgb_to_grayscale (float input): 0.2989 r + 0.587 g + 0.114 b
-    r, g, b = img[0], img[1], img[2]
-    return (F32(0.2989) * r + F32(0.587) * g + F32(0.114) * b).astype(F32)
-
-
-def _blend(img1, img2, ratio, one_minus):
-    return np.clip(F32(ratio) * img1 + F32(one_minus) * img2, F32(0), F32(1)).astype(F32)
-
-
-def _rgb2hsv(img):
-    r, g, b = img[0], img[1], img[2]
-    maxc = img.max(axis=0)
-    minc = img.min(axis=0)
-    eqc = maxc == minc
-    cr = maxc - minc
-    ones = np.ones_like(maxc)
-    s = cr / np.where(eqc, ones, maxc)
-    crd = np.where(eqc, ones, cr)
-    rc = (maxc - r) / crd
-    gc = (maxc - g) / crd
-    bc = (maxc - b) / crd
-    hr = (maxc == r) * (bc - gc)
-    hg = ((maxc == g) & (maxc != r)) * (F32(2.0) + rc - bc)
-    hb = ((maxc != g) & (maxc != r)) * (F32(4.0) + gc - rc)
-    h = (hr + hg + hb).astype(F32)
-    h = np.fmod(h / F32(6.0) + F32(1.0), F32(1.0)).astype(F32)
-    return np.stack((h, s.astype(F32), maxc))
-
-
-def _hsv2rgb(img):
-    h, s, v = img[0], img[1], img[2]
-    i = np.floor(h * F32(6.0))
-    f = (h * F32(6.0) - i).astype(F32)
-    i = i.astype(np.int32) % 6
-    p = np.clip(v * (F32(1.0) - s), 0, 1).astype(F32)
-    q = np.clip(v * (F32(1.0) - s * f), 0, 1).astype(F32)
-    t = np.clip(v * (F32(1.0) - s * (F32(1.0) - f)), 0, 1).astype(F32)
-    r = np.choose(i, (v, q, p, p, t, v))
-    g = np.choose(i, (t, v, v, q, p, p))
-    b = np.choose(i, (p, p, t, v, v, q))
-    return np.stack((r, g, b)).astype(F32)
-
-
-def jitter_tensor(img, prm):
-    """ColorJitter.forward on a float32 [3, H, W] image in [0, 1] (functional_tensor)."""
-    bf, cf, sf, hf = (float(x) for x in prm[1:5])
-    c1, s1 = (float(x) for x in prm[9:11])
-    for fn in prm[5:9].astype(int):
-        if fn == 0:
-            img = _blend(img, np.zeros_like(img), bf, 1.0 - bf)
-        elif fn == 1:
-            m = F32(_gray(img).mean(dtype=np.float64))
-            img = _blend(img, m, cf, c1)
-        elif fn == 2:
-            img = _blend(img, _gray(img)[None], sf, s1)
-        else:
-            hsv = _rgb2hsv(img)
-            h = (hsv[0] + F32(hf)).astype(F32)
-            hsv[0] = h - np.floor(h)
-            img = _hsv2rgb(hsv)
-    return img
-
-
-def augment_tensor(u8, params):
-    """u8 [B, H, W, 3] uint8, params [B, 12] -> float32 [B, 3, H, W] in [-1, 1]."""
-    out = []
-    for im, prm in zip(u8, params):
-        x = im.transpose(2, 0, 1).astype(F32) / F32(255.0)      # ToTensor (div by 255)
-        if prm[0]:
-            x = x[:, :, ::-1]                                     # hflip
-        x = jitter_tensor(np.ascontiguousarray(x), prm)
-        out.append(((x - F32(0.5)) / F32(0.5)).astype(F32))       # Normalize
-    return np.stack(out)
+def hue_shift_u8(hf):
+    """np.uint8(hue_factor * 255): the product in double, truncated, wrapped to a byte."""
+    return int(np.array(float(hf) * 255.0).astype(np.int64)) & 255
 
 
 def augment_pil(u8, params):
-    """The reference's path: flip + the four ops on the PIL image, then ToTensor +
-    Normalize (functional_pil.adjust_* as torchvision applies them)."""
+    """The reference's path: flip + the four ops on the PIL image (functional_pil), then
+    ToTensor (uint8 / 255 in fp32) + Normalize."""
     from PIL import Image, ImageEnhance
     out = []
     for im, prm in zip(u8, params):
@@ -124,8 +56,99 @@ def augment_pil(u8, params):
                 h, s, v = img.convert("HSV").split()
                 np_h = np.array(h, dtype=np.uint8)
                 with np.errstate(over="ignore"):
-                    np_h += np.array(hf * 255).astype(np.int64).astype(np.uint8)
+                    np_h += np.uint8(hue_shift_u8(hf))
                 img = Image.merge("HSV", (Image.fromarray(np_h, "L"), s, v)).convert("RGB")
         x = np.asarray(img, F32).transpose(2, 0, 1) / F32(255.0)
         out.append((x - F32(0.5)) / F32(0.5))
+    return np.stack(out)
+
+
+# ---- numpy restatement of Pillow's C arithmetic (libImaging) --------------------------
+def blend_u8(a, b, alpha):
+    """ImagingBlend (Blend.c): out = in1 + alpha * (in2 - in1) in float (alpha is the C
+    float of the factor), truncated to uint8; outside 0 <= alpha <= 1 clipped to [0, 255]."""
+    al = F32(alpha)
+    t = (np.asarray(a).astype(F32) + al * (np.asarray(b).astype(F32) - np.asarray(a).astype(F32))
+         ).astype(F32)
+    if F32(0) <= al <= F32(1):
+        return t.astype(np.int64)
+    return np.where(t <= 0, 0, np.where(t >= 255, 255, np.trunc(t))).astype(np.int64)
+
+
+def luma_u8(r, g, b):
+    """rgb2l (Convert.c): ITU-R 601-2 luma in 16.16 fixed point, rounded."""
+    return (r * 19595 + g * 38470 + b * 7471 + 0x8000) >> 16
+
+
+def rgb2hsv_u8(r, g, b):
+    """rgb2hsv_row (Convert.c): float ratios, the sector offsets and the wrap in double,
+    truncation to uint8; max == min gives h = s = 0."""
+    mx = np.maximum(r, np.maximum(g, b))
+    mn = np.minimum(r, np.minimum(g, b))
+    eq = mx == mn
+    cr = np.where(eq, 1, mx - mn).astype(F32)
+    s = cr / np.where(mx == 0, 1, mx).astype(F32)
+    rc = (mx - r).astype(F32) / cr
+    gc = (mx - g).astype(F32) / cr
+    bc = (mx - b).astype(F32) / cr
+    h = np.where(r == mx, (bc - gc).astype(F64),
+                 np.where(g == mx, (2.0 + rc.astype(F64)) - bc.astype(F64),
+                          (4.0 + gc.astype(F64)) - rc.astype(F64))).astype(F32)
+    h = np.fmod(h.astype(F64) / 6.0 + 1.0, 1.0).astype(F32)
+    uh = np.clip((h.astype(F64) * 255.0).astype(np.int64), 0, 255)
+    us = np.clip((s.astype(F64) * 255.0).astype(np.int64), 0, 255)
+    return np.where(eq, 0, uh), np.where(eq, 0, us), mx
+
+
+def hsv2rgb_u8(h, s, v):
+    """hsv2rgb (Convert.c): sector and remainder in double, fs and f stored as float, C
+    round() (half away from zero) of v * (1 - ...), clipped; s == 0 gives (v, v, v)."""
+    hd = h.astype(F32).astype(F64) * 6.0 / 255.0
+    i = np.floor(hd).astype(np.int64)
+    f = (hd - i.astype(F32).astype(F64)).astype(F32)
+    fs = (s.astype(F32).astype(F64) / 255.0).astype(F32)
+    vf = v.astype(F32).astype(F64)
+
+    def c8(x):
+        return np.clip(np.floor(x + 0.5), 0, 255).astype(np.int64)
+    p = c8(vf * (1.0 - fs.astype(F64)))
+    q = c8(vf * (1.0 - (fs * f).astype(F32).astype(F64)))
+    t = c8(vf * (1.0 - fs.astype(F64) * (1.0 - f.astype(F64))))
+    k = i % 6
+    R = np.choose(k, (v, q, p, p, t, v))
+    G = np.choose(k, (t, v, v, q, p, p))
+    B = np.choose(k, (p, p, t, v, v, q))
+    z = s == 0
+    return np.where(z, v, R), np.where(z, v, G), np.where(z, v, B)
+
+
+def contrast_mean(r, g, b):
+    """ImageEnhance.Contrast's degenerate level: int(ImageStat.Stat(L).mean[0] + 0.5), the
+    mean = (exact integer sum of L) / count in double."""
+    L = luma_u8(r, g, b)
+    return int(float(L.sum()) / float(L.size) + 0.5)
+
+
+def augment_pil_np(u8, params):
+    """augment_pil with every op restated (what pg_augment_u8 computes)."""
+    out = []
+    for im, prm in zip(u8, params):
+        x = im[:, ::-1] if prm[0] else im
+        r, g, b = (x[..., c].astype(np.int64) for c in range(3))
+        bf, cf, sf = F32(prm[1]), F32(prm[2]), F32(prm[3])
+        dh = hue_shift_u8(prm[4])
+        for fn in prm[5:9].astype(int):
+            if fn == 0:
+                r, g, b = blend_u8(0, r, bf), blend_u8(0, g, bf), blend_u8(0, b, bf)
+            elif fn == 1:
+                m = contrast_mean(r, g, b)
+                r, g, b = blend_u8(m, r, cf), blend_u8(m, g, cf), blend_u8(m, b, cf)
+            elif fn == 2:
+                L = luma_u8(r, g, b)
+                r, g, b = blend_u8(L, r, sf), blend_u8(L, g, sf), blend_u8(L, b, sf)
+            else:
+                h, s, v = rgb2hsv_u8(r, g, b)
+                r, g, b = hsv2rgb_u8((h + dh) & 255, s, v)
+        y = np.stack([r, g, b]).astype(F32) / F32(255.0)
+        out.append((y - F32(0.5)) / F32(0.5))
     return np.stack(out)

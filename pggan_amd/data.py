@@ -12,10 +12,9 @@ batch (three launches).  The random parameters are drawn on the host with a torc
 generator in torchvision's call order per image -- `torch.rand(1) < p` for the flip, then
 ColorJitter.get_params: `torch.randperm(4)`, brightness, contrast, saturation, hue
 `torch.empty(1).uniform_(lo, hi)` -- so a generator in the same state draws the same
-parameters as the reference's transform.  The jitter arithmetic is torchvision's tensor
-formulation in fp32; the reference applies the same four ops to the PIL image (uint8
-rounding after each op), which differs by a few /255 per pixel (tests/test_augment.py
-measures it against a PIL-path restatement).
+parameters as the reference's transform.  The jitter is the reference's PIL path
+(ImageEnhance blends and PIL's uint8 HSV hue shift, uint8 after every op) in Pillow's own
+arithmetic: the output equals the reference transform byte for byte (tests/test_augment.py).
 """
 from __future__ import annotations
 
@@ -53,7 +52,7 @@ def load_u8(path, size):
 def draw_params(B, gen):
     """Per-image flip / ColorJitter parameters in torchvision's draw order -> fp32 [B, 12]:
     {flip, brightness, contrast, saturation, hue, fn_idx[4], 1 - contrast, 1 - saturation, 0}
-    (1 - factor computed in double, as torchvision's _blend does)."""
+    (the last three are not read by the PIL-path kernel; the table layout is the ABI's)."""
     p = np.zeros((B, PSTRIDE), np.float32)
     for b in range(B):
         flip = bool(torch.rand(1, generator=gen) < FLIP_P)
