@@ -319,8 +319,8 @@ def main():
 
     log = lambda m: print(f"[bench] {m}", file=sys.stderr, flush=True)
     log(f"stage {s} batch {B} world {world}: {args.warmup} warm-up steps")
-    # one process: from the second step on, train_step replays the step captured as a
-    # hipGraph (ProgressiveGAN.use_graph; PG_GRAPH=0 keeps it eager)
+    # PG_GRAPH=1 (one process): from the second step on, train_step replays the step
+    # captured as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
     for _ in range(args.warmup):
         step()
     model.flush()

@@ -187,6 +187,36 @@ int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, cons
 int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
                     float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
                     void* stream);
+/* An image operand of the fromRGB layers given as a per-sample mix instead of a tensor:
+ * img[b] = a[b] * x0[b] + c[b] * x1[b] (NCHW fp32; a, c: DEVICE arrays of B floats; x1 and c
+ * may be NULL; a == NULL means img = x0).  The gradient-penalty passes read the interpolated
+ * image eps x_real + (1 - eps) x_fake (pggan/loss.py:75) and the penalty-weighted input
+ * gradient this way, so neither is materialised. */
+typedef struct {
+  const float* x0;
+  const float* x1;
+  const float* a;
+  const float* c;
+} pg_img_src;
+/* pg_from_rgb with the image operand as a pg_img_src */
+int pg_from_rgb_src(int dtype, int B, int R, int C, const pg_img_src* img, int down, const float* w,
+                    const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
+                    void* stream);
+/* pg_from_rgb_bwd with the image operand (of the weight gradient) as a pg_img_src, and for the
+ * input gradient: gimg_overwrite = 1 writes gimg instead of accumulating into it; norms !=
+ * NULL: norms[b] += sum over sample b of the final gimg^2 (the penalties' per-sample squared
+ * norms, fused into the pass that writes the input gradient) */
+int pg_from_rgb_bwd_src(int dtype, int B, int R, int C, const pg_img_src* img, int down,
+                        const float* w, float c, int gz_cs, const void* gz, float* gimg,
+                        int gimg_overwrite, float* norms, float* dw, float* db, void* stream);
+/* The penalty and the tangent-pass scale from the per-sample squared norms n_b of g = dD/dx:
+ * mode 0 (R1, lib/loss.py:125-135): loss_out[0] += 0.5 * sum_b n_b / B, scale_b = 1 / B;
+ * mode 1 (WGAN-GP, pggan/loss.py:81-87): loss_out[0] += w * sum_b (sqrt(n_b) - 1)^2,
+ * scale_b = 2 w (sqrt(n_b) - 1) / sqrt(n_b) (0 where n_b = 0).  scale: DEVICE [B].  The
+ * norms are reset to 0 (ready for the next accumulating pass: no memset per step). */
+int pg_penalty_scale(int mode, int B, float* norms, float w, float* loss_out, float* scale,
+                     void* stream);
+
 /* real-image fade (pggan/model.py:217-221): out = (1-a)*up2(avgpool2(x)) + a*x, NCHW fp32 */
 int pg_img_fade(int B, int C, int R, const float* x, float alpha, float* out, void* stream);
 

@@ -45,6 +45,38 @@ def _cinp(c):
     return (c + 7) // 8 * 8 if c <= 16 else (c + 31) // 32 * 32
 
 
+class ImgMix:
+    """An image operand given as a per-sample mix (pg_img_src): img[b] = a[b] * x0[b] +
+    c[b] * x1[b] (x1 / c optional; a None means x0 itself).  The penalty passes feed the
+    fromRGB layers the interpolated image and the weighted input gradient this way."""
+
+    def __init__(self, x0, x1=None, a=None, c=None):
+        self.x0, self.x1, self.a, self.c = x0, x1, a, c
+
+    @property
+    def shape(self):
+        return self.x0.shape
+
+    @property
+    def device(self):
+        return self.x0.device
+
+    def materialize(self):
+        """The mixed image as a tensor (the CPU test double; never the HIP path)."""
+        if self.a is None:
+            return self.x0
+        v = self.a.view(-1, 1, 1, 1) * self.x0
+        if self.x1 is not None:
+            v = v + self.c.view(-1, 1, 1, 1) * self.x1
+        return v
+
+
+class ImgSrcDesc(ctypes.Structure):
+    """pg_img_src (include/pggan_hip.h)."""
+    _fields_ = [("x0", ctypes.c_void_p), ("x1", ctypes.c_void_p), ("a", ctypes.c_void_p),
+                ("c", ctypes.c_void_p)]
+
+
 class LinearDesc(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("B", "K", "N", "in_cs", "out_cs", "flags")] + \
                [("scale", ctypes.c_float), ("slope", ctypes.c_float)]
@@ -83,6 +115,11 @@ _SIGS = {
     "pg_from_rgb": ([_I, _I, _I, _I, _VP, _I, _VP, _VP, _F, _F, _VP, _I, _VP, _VP], _I),
     "pg_from_rgb_bwd": ([_I, _I, _I, _I, _VP, _I, _VP, _F, _I, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_img_fade": ([_I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_from_rgb_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP, _I,
+                         _VP, _VP], _I),
+    "pg_from_rgb_bwd_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _F, _I, _VP, _VP,
+                             _I, _VP, _VP, _VP, _VP], _I),
+    "pg_penalty_scale": ([_I, _I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_linear_fwd": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_linear_dgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
     "pg_linear_wgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
@@ -324,17 +361,43 @@ class HipOps:
                                           alpha, _p(gimg), _p(gx), _p(gxp), _p(dw), _p(db), _p(dwp),
                                           _p(dbp), self._s()), "rgb_out_bwd")
 
-    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
-        self._cuda(img, w, b, y, mask_y)
-        self._chk(self.lib.pg_from_rgb(self._dt(y), B, R, C, _p(img), 1 if down else 0, _p(w), _p(b),
-                                       c, slope, _p(mask_y), y.shape[-1], _p(y), self._s()),
-                  "from_rgb")
+    def _src(self, img):
+        """pg_img_src of an image operand (a tensor or an ImgMix)."""
+        if img is None:
+            return None
+        if isinstance(img, ImgMix):
+            self._cuda(img.x0, img.x1, img.a, img.c)
+            return ImgSrcDesc(img.x0.data_ptr(), img.x1.data_ptr() if img.x1 is not None else None,
+                              img.a.data_ptr() if img.a is not None else None,
+                              img.c.data_ptr() if img.c is not None else None)
+        self._cuda(img)
+        return ImgSrcDesc(img.data_ptr(), None, None, None)
 
-    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None):
-        self._cuda(gz, w, img, gimg, dw, db)
-        self._chk(self.lib.pg_from_rgb_bwd(self._dt(gz), B, R, C, _p(img), 1 if down else 0, _p(w),
-                                           c, gz.shape[-1], _p(gz), _p(gimg), _p(dw), _p(db),
-                                           self._s()), "from_rgb_bwd")
+    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
+        self._cuda(w, b, y, mask_y)
+        src = self._src(img)
+        self._chk(self.lib.pg_from_rgb_src(self._dt(y), B, R, C, ctypes.byref(src), 1 if down else 0,
+                                           _p(w), _p(b), c, slope, _p(mask_y), y.shape[-1], _p(y),
+                                           self._s()), "from_rgb")
+
+    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None,
+                     gimg_overwrite=False, norms=None):
+        """gimg_overwrite: write gimg instead of accumulating into it; norms: += per-sample sum
+        of squares of the final gimg (the penalties' squared norms)."""
+        self._cuda(gz, w, gimg, dw, db, norms)
+        src = self._src(img)
+        self._chk(self.lib.pg_from_rgb_bwd_src(self._dt(gz), B, R, C,
+                                               ctypes.byref(src) if src is not None else None,
+                                               1 if down else 0, _p(w), c, gz.shape[-1], _p(gz),
+                                               _p(gimg), 1 if gimg_overwrite else 0, _p(norms),
+                                               _p(dw), _p(db), self._s()), "from_rgb_bwd")
+
+    def penalty_scale(self, mode, norms, w, loss, scale):
+        """mode "r1" / "wgan-gp": the penalty into loss[0] and the per-sample tangent scale
+        from the squared norms (pg_penalty_scale)."""
+        self._cuda(norms, loss, scale)
+        self._chk(self.lib.pg_penalty_scale(0 if mode == "r1" else 1, norms.numel(), _p(norms), w,
+                                            _p(loss), _p(scale), self._s()), "penalty_scale")
 
     def img_fade(self, x, alpha, out):
         self._cuda(x, out)

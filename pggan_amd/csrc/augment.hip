@@ -22,7 +22,7 @@
 
 #include "common.h"
 
-#pragma clang fp contract(off)
+#pragma clang fp contract(off)   // and -ffp-contract=off for this file (Makefile)
 
 namespace {
 

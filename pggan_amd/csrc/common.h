@@ -64,6 +64,36 @@ template <> struct Ty<bf16_t> {
   }
 };
 
+// Image operand of the fromRGB kernels (NCHW fp32 [B][3][Ri][Ri]): x0, or per sample b the
+// mix a[b] * x0 + c[b] * x1 (x1 / c may be NULL: a scaled image).  The gradient-penalty
+// passes read the interpolated image eps x_real + (1 - eps) x_fake and the scaled input
+// gradient through it instead of materialising them (pg_img_src in the C ABI).
+struct ImgSrc {
+  const float* x0;
+  const float* x1;
+  const float* a;
+  const float* c;
+  __host__ __device__ ImgSrc(const float* p = nullptr) : x0(p), x1(nullptr), a(nullptr), c(nullptr) {}
+  __host__ ImgSrc(const pg_img_src& s) : x0(s.x0), x1(s.x1), a(s.a), c(s.c) {}
+  __host__ __device__ explicit operator bool() const { return x0 != nullptr; }
+  // separate roundings (no contraction): a * x0 + c * x1 as the reference's fp32 tensor ops
+  __device__ __forceinline__ float mix(int b, float v0, float v1) const {
+    float v = __fmul_rn(a[b], v0);
+    if (x1) v = __fadd_rn(v, __fmul_rn(c[b], v1));
+    return v;
+  }
+  __device__ __forceinline__ float at(int b, size_t i) const {
+    if (!a) return x0[i];
+    return mix(b, x0[i], x1 ? x1[i] : 0.f);
+  }
+  __device__ __forceinline__ float2 at2(int b, size_t i) const {
+    const float2 u = *reinterpret_cast<const float2*>(x0 + i);
+    if (!a) return u;
+    const float2 t = x1 ? *reinterpret_cast<const float2*>(x1 + i) : make_float2(0.f, 0.f);
+    return make_float2(mix(b, u.x, t.x), mix(b, u.y, t.y));
+  }
+};
+
 __device__ __forceinline__ float lrelu_f(float v, float slope) { return v > 0.f ? v : v * slope; }
 __device__ __forceinline__ float lmask_f(float y, float slope) { return y > 0.f ? 1.f : slope; }
 

@@ -371,24 +371,24 @@ __global__ __launch_bounds__(256) void rgb_wgrad_small(int B, int Rx, int x_cs, 
   block_reduce_atomic<3 * C + 3, 3 * C>(acc, red, dw, db, f);
 }
 
-__device__ __forceinline__ void img_in3(const float* img, int bi, int R, int py, int px, int down,
+__device__ __forceinline__ void img_in3(const ImgSrc& img, int bi, int R, int py, int px, int down,
                                         float v[3]) {
   if (!down) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) v[i] = img[(((size_t)bi * 3 + i) * R + py) * R + px];
+    for (int i = 0; i < 3; ++i) v[i] = img.at(bi, (((size_t)bi * 3 + i) * R + py) * R + px);
   } else {
     const int Ri = 2 * R;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const float* p = img + ((size_t)bi * 3 + i) * Ri * Ri;
-      const size_t a = (size_t)(2 * py) * Ri + 2 * px;
-      v[i] = 0.25f * (p[a] + p[a + 1] + p[a + Ri] + p[a + Ri + 1]);
+      const size_t p = ((size_t)bi * 3 + i) * Ri * Ri;
+      const size_t a = p + (size_t)(2 * py) * Ri + 2 * px;
+      v[i] = 0.25f * (img.at(bi, a) + img.at(bi, a + 1) + img.at(bi, a + Ri) + img.at(bi, a + Ri + 1));
     }
   }
 }
 
 template <typename T>
-__global__ void from_rgb_kernel(int B, int R, int C, const float* img, int down, const float* w,
+__global__ void from_rgb_kernel(int B, int R, int C, ImgSrc img, int down, const float* w,
                                 const float* b, float c, float slope, const T* mask_y, int y_cs,
                                 T* y) {
   const int nv = C >> 2;
@@ -420,15 +420,19 @@ __global__ void from_rgb_kernel(int B, int R, int C, const float* img, int down,
   }
 }
 
-// gimg (at the input resolution) += c * sum_o gz[pix_out][o] W[o][i] (* 0.25 if down)
+// gimg (at the input resolution) += c * sum_o gz[pix_out][o] W[o][i] (* 0.25 if down); ow:
+// gimg = (no accumulation); norms: norms[b] += sum of the final gimg^2 of sample b.  grid =
+// (ceil(Ri / 256), B * Ri): a block is 256 pixels of one image row (one sample)
 template <typename T>
-__global__ void from_rgb_dgrad_kernel(int B, int R, int C, int down, const float* w, float c,
-                                      int gz_cs, const T* gz, float* gimg) {
+__global__ __launch_bounds__(256) void from_rgb_dgrad_kernel(int R, int C, int down, const float* w,
+                                                             float c, int gz_cs, const T* gz,
+                                                             float* gimg, int ow, float* norms) {
   const int Ri = down ? 2 * R : R;
-  const size_t n = (size_t)B * Ri * Ri;
   const float f = down ? 0.25f * c : c;
-  GRID_STRIDE(i, n) {
-    const int px = (int)(i % Ri), py = (int)((i / Ri) % Ri), bi = (int)(i / ((size_t)Ri * Ri));
+  const int px = blockIdx.x * 256 + threadIdx.x;
+  const int row = blockIdx.y, bi = row / Ri, py = row - bi * Ri;
+  float q = 0.f;
+  if (px < Ri) {
     const int qy = down ? py >> 1 : py, qx = down ? px >> 1 : px;
     const T* gp = gz + (((size_t)bi * R + qy) * R + qx) * gz_cs;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
@@ -444,15 +448,24 @@ __global__ void from_rgb_dgrad_kernel(int B, int R, int C, int down, const float
     }
     const size_t plane = (size_t)Ri * Ri;
     float* dst = gimg + (size_t)bi * 3 * plane + (size_t)py * Ri + px;
-    dst[0] += f * s0;
-    dst[plane] += f * s1;
-    dst[2 * plane] += f * s2;
+    const float v0 = ow ? f * s0 : dst[0] + f * s0;
+    const float v1 = ow ? f * s1 : dst[plane] + f * s1;
+    const float v2 = ow ? f * s2 : dst[2 * plane] + f * s2;
+    dst[0] = v0;
+    dst[plane] = v1;
+    dst[2 * plane] = v2;
+    q = v0 * v0 + v1 * v1 + v2 * v2;
+  }
+  if (norms) {   // uniform
+    __shared__ float red[4];
+    const float t = block_sum(q, red);
+    if (threadIdx.x == 0) atomicAdd(norms + bi, t);
   }
 }
 
 // dw[o][i] += c * sum_pix gz[pix][o] img_in[i][pix]; db[o] += c * sum gz[pix][o]
 template <typename T>
-__global__ void from_rgb_wgrad_kernel(int B, int R, int C, const float* img, int down, float c,
+__global__ void from_rgb_wgrad_kernel(int B, int R, int C, ImgSrc img, int down, float c,
                                       int gz_cs, const T* gz, float* dw, float* db,
                                       int pix_per_block) {
   __shared__ float red[256 * 4];
@@ -503,7 +516,7 @@ __global__ void from_rgb_wgrad_kernel(int B, int R, int C, const float* img, int
 
 // fromRGB wgrad for small C: dw[o][i] += c sum gz[pix][o] img_in[i][pix], db[o] += c sum gz
 template <typename T, int C>
-__global__ __launch_bounds__(256) void from_rgb_wgrad_small(int B, int R, const float* img, int down, float c,
+__global__ __launch_bounds__(256) void from_rgb_wgrad_small(int B, int R, ImgSrc img, int down, float c,
                                      int gz_cs, const T* gz, float* dw, float* db) {
   __shared__ float red[4 * 4 * C];
   const size_t npix = (size_t)B * R * R;
@@ -1076,6 +1089,27 @@ __global__ void gp_finish_kernel(int B, size_t per, const float* g, float w, con
   }
 }
 
+// the penalty from the per-sample squared norms n_b and the tangent pass's per-sample scale
+// (pg_penalty_scale): one thread, B small
+__global__ void penalty_scale_kernel(int mode, int B, float* norms, float w, float* loss,
+                                     float* scale) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float t = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float n = norms[b];
+    norms[b] = 0.f;   // ready for the next pass that accumulates them
+    if (mode == 0) {
+      t += n;
+      scale[b] = 1.f / (float)B;
+    } else {
+      const float nb = sqrtf(n);
+      t += (nb - 1.f) * (nb - 1.f);
+      scale[b] = nb > 0.f ? w * 2.f * (nb - 1.f) / nb : 0.f;
+    }
+  }
+  loss[0] += mode == 0 ? 0.5f * t / (float)B : w * t;
+}
+
 __global__ void mul_add_kernel(size_t n, const float* x, const float* y, const float* z, float* out) {
   GRID_STRIDE(i, n) out[i] = x[i] + y[i] * z[i];
 }
@@ -1411,12 +1445,11 @@ int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, cons
                               wp, cp, alpha, gimg, (bf16_t*)gx, (bf16_t*)gxp, dw, db, dwp, dbp, st);
 }
 
-int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
-                const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
-                void* stream) {
+static int from_rgb_impl(int dtype, int B, int R, int C, const ImgSrc& img, int down,
+                         const float* w, const float* b, float c, float slope, const void* mask_y,
+                         int y_cs, void* y, hipStream_t st) {
   PG_CHECK_ARG(img && w && y && C % 4 == 0 && y_cs >= C, "from_rgb: bad args");
   const size_t n = (size_t)B * R * R * (C / 4);
-  hipStream_t st = (hipStream_t)stream;
   if ((dtype == PG_F32 ? try_from_rgb<float>(B, R, C, img, down, w, b, c, slope, (const float*)mask_y,
                                              y_cs, (float*)y, st)
                        : try_from_rgb<bf16_t>(B, R, C, img, down, w, b, c, slope,
@@ -1434,28 +1467,43 @@ int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, cons
   return PG_OK;
 }
 
-int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
-                    float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
+int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
+                void* stream) {
+  return from_rgb_impl(dtype, B, R, C, ImgSrc(img), down, w, b, c, slope, mask_y, y_cs, y,
+                       (hipStream_t)stream);
+}
+
+int pg_from_rgb_src(int dtype, int B, int R, int C, const pg_img_src* img, int down, const float* w,
+                    const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
                     void* stream) {
+  PG_CHECK_ARG(img && (!img->x1 || (img->a && img->c)), "from_rgb_src: bad image source");
+  return from_rgb_impl(dtype, B, R, C, ImgSrc(*img), down, w, b, c, slope, mask_y, y_cs, y,
+                       (hipStream_t)stream);
+}
+
+static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, int down,
+                             const float* w, float c, int gz_cs, const void* gz, float* gimg, int ow,
+                             float* norms, float* dw, float* db, hipStream_t st) {
   PG_CHECK_ARG(w && gz && C % 4 == 0, "from_rgb_bwd: bad args");
   PG_CHECK_ARG(!(dw || db) || img, "from_rgb_bwd: wgrad needs img");
-  hipStream_t st = (hipStream_t)stream;
+  PG_CHECK_ARG(!norms || gimg, "from_rgb_bwd: norms need gimg");
   if ((dtype == PG_F32 ? try_from_rgb_bwd<float>(B, R, C, img, down, w, c, gz_cs, (const float*)gz,
-                                                 gimg, dw, db, st)
+                                                 gimg, ow, norms, dw, db, st)
                        : try_from_rgb_bwd<bf16_t>(B, R, C, img, down, w, c, gz_cs,
-                                                  (const bf16_t*)gz, gimg, dw, db, st)) == 0) {
+                                                  (const bf16_t*)gz, gimg, ow, norms, dw, db, st)) == 0) {
     PG_LAUNCH_CHECK();
     return PG_OK;
   }
   if (gimg) {
     const int Ri = down ? 2 * R : R;
-    const size_t n = (size_t)B * Ri * Ri;
+    const dim3 grid((Ri + 255) / 256, B * Ri);
     if (dtype == PG_F32)
-      hipLaunchKernelGGL(from_rgb_dgrad_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C,
-                         down, w, c, gz_cs, (const float*)gz, gimg);
+      hipLaunchKernelGGL(from_rgb_dgrad_kernel<float>, grid, dim3(256), 0, st, R, C, down, w, c,
+                         gz_cs, (const float*)gz, gimg, ow, norms);
     else
-      hipLaunchKernelGGL(from_rgb_dgrad_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R,
-                         C, down, w, c, gz_cs, (const bf16_t*)gz, gimg);
+      hipLaunchKernelGGL(from_rgb_dgrad_kernel<bf16_t>, grid, dim3(256), 0, st, R, C, down, w, c,
+                         gz_cs, (const bf16_t*)gz, gimg, ow, norms);
   }
   if (dw || db) {
     const size_t npix = (size_t)B * R * R;
@@ -1485,6 +1533,31 @@ int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, 
                            img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
     }
   }
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
+                    float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
+                    void* stream) {
+  return from_rgb_bwd_impl(dtype, B, R, C, ImgSrc(img), down, w, c, gz_cs, gz, gimg, 0, nullptr,
+                           dw, db, (hipStream_t)stream);
+}
+
+int pg_from_rgb_bwd_src(int dtype, int B, int R, int C, const pg_img_src* img, int down,
+                        const float* w, float c, int gz_cs, const void* gz, float* gimg,
+                        int gimg_overwrite, float* norms, float* dw, float* db, void* stream) {
+  PG_CHECK_ARG(!img || !img->x1 || (img->a && img->c), "from_rgb_bwd_src: bad image source");
+  return from_rgb_bwd_impl(dtype, B, R, C, img ? ImgSrc(*img) : ImgSrc(), down, w, c, gz_cs, gz,
+                           gimg, gimg_overwrite, norms, dw, db, (hipStream_t)stream);
+}
+
+int pg_penalty_scale(int mode, int B, float* norms, float w, float* loss_out, float* scale,
+                     void* stream) {
+  PG_CHECK_ARG(norms && loss_out && scale && B > 0 && (mode == 0 || mode == 1),
+               "penalty_scale: bad args");
+  hipLaunchKernelGGL(penalty_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mode, B, norms,
+                     w, loss_out, scale);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

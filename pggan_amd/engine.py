@@ -347,7 +347,11 @@ class StepEngine:
             # WGAN-GP optional mode
             D["interp"] = t(B, 3, R, R, f32=True)
             D["gp_eps"] = t(B, 1, f32=True)
+            D["gp_c"] = t(B, 1, f32=True)         # 1 - eps
+            # per-sample squared norms of dD/dx (kept at zero between uses: pg_penalty_scale
+            # resets them) and the tangent pass's per-sample scale of dD/dx
             D["gp_norms"] = t(B, f32=True)
+            D["gp_scale"] = t(B, f32=True)
             D["ones"] = torch.full((B,), 1.0, dtype=torch.float32, device=self.dev)
             D["zeros"] = torch.zeros((B,), dtype=torch.float32, device=self.dev)
         return D
@@ -720,9 +724,13 @@ class StepEngine:
         with torch.cuda.stream(self.side):
             self.grad_ready(net, names)
 
-    def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False):
+    def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False,
+                   gimg_overwrite=False, norms=None):
         """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
-        gimg: accumulate dL/dimg (must be zeroed by the caller); keeps every gz.
+        gimg: accumulate dL/dimg (zeroed by the caller unless gimg_overwrite: the first
+        fromRGB input gradient then writes it); norms: += per-sample sum of dL/dimg^2, fused
+        into the last pass writing gimg; keeps every gz.  img: the D input (a tensor or an
+        _lib.ImgMix) for the fromRGB weight gradients.
         final: the last pass writing D's gradients this half-step (grad_ready calls)."""
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
         self._side_join("D")
@@ -806,7 +814,8 @@ class StepEngine:
                             dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
             ready(fr.format(s))
         if gimg is not None:
-            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg)
+            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg,
+                             **self._gimg_kw(gimg_overwrite, None if low else norms))
         if low:
             w1 = P[fr.format(s - 1) + "weight"]
             if GR is not None:
@@ -817,7 +826,38 @@ class StepEngine:
                 ready(fr.format(s - 1))
             if gimg is not None:
                 ops.from_rgb_bwd(D["gzd"], w1, he(3), B=B, R=R // 2, C=d[s - 1], down=True,
-                                 gimg=gimg)
+                                 gimg=gimg, **self._gimg_kw(False, norms))
+
+    @staticmethod
+    def _gimg_kw(overwrite, norms):
+        kw = {}
+        if overwrite:
+            kw["gimg_overwrite"] = True
+        if norms is not None:
+            kw["norms"] = norms
+        return kw
+
+    def _fused_penalty(self):
+        """The penalties' squared norms fused into the input-gradient pass and their weighted
+        gradient read by the tangent pass through an image mix (the ops support it)."""
+        return hasattr(self.ops, "penalty_scale")
+
+    def _input_grad(self, P, u, alpha, mode, w=0.0):
+        """B1 of a penalty: dD/dx into D["gimg"] from the upstream u, the penalty into
+        loss[2] and the tangent pass's input gbar (R1: g / B; WGAN-GP: the weighted g)."""
+        ops, D, B = self.ops, self.dd, self.B
+        if self._fused_penalty():
+            self.d_backward(P, None, u, alpha, gimg=D["gimg"], gimg_overwrite=True,
+                            norms=D["gp_norms"])
+            ops.penalty_scale(mode, D["gp_norms"], w, self.loss[2:3], D["gp_scale"])
+            return L.ImgMix(D["gimg"], a=D["gp_scale"])
+        D["gimg"].zero_()
+        self.d_backward(P, None, u, alpha, gimg=D["gimg"])
+        if mode == "r1":
+            ops.r1_penalty(D["gimg"], B, self.loss[2:3], D["gbar"])   # lib/loss.py:125-135
+        else:
+            ops.gp_penalty(D["gimg"], w, self.loss[2:3], D["gp_norms"], D["gbar"])
+        return D["gbar"]
 
     def d_tangent(self, P, GR, gbar, u, alpha):
         """Push gbar (= dR1/dx-gradient) forward through D with the B1 masks, adding the R1
@@ -904,10 +944,8 @@ class StepEngine:
             # ---- real: F, B1, R1, T, B2
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], D["hl"])   # lib/loss.py:119-123
-            D["gimg"].zero_()
-            self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
-            ops.r1_penalty(D["gimg"], B, self.loss[2:3], D["gbar"])          # lib/loss.py:125-135
-            tout, inj = self.d_tangent(PD, GD, D["gbar"], D["u"], alpha_D)
+            gbar = self._input_grad(PD, D["u"], alpha_D, "r1")                # lib/loss.py:125-135
+            tout, inj = self.d_tangent(PD, GD, gbar, D["u"], alpha_D)
             ops.mul_add(D["u"], tout.view(-1), D["hl"], D["u2"])
             self.d_backward(PD, GD, D["u2"], alpha_D, img=xr, inj_mbstd=inj)
             if conc:
@@ -972,17 +1010,24 @@ class StepEngine:
         return img_fake
 
     def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
-        """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm."""
+        """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm.
+        Fused form: the interpolation eps x_r + (1 - eps) x_f is read by the fromRGB layers
+        from x_r, x_f and eps (never written), the per-sample squared norm is summed by the
+        pass writing dD/dx, and the tangent pass reads dD/dx with the per-sample weight
+        2 W_gp (|g| - 1) / |g| applied on load."""
         ops, D, B = self.ops, self.dd, self.B
         D["gp_eps"].copy_(eps)
-        ops.gp_interp(xr, xf, D["gp_eps"], D["interp"])
-        self.d_forward(PD, D["interp"], alpha)
-        D["gimg"].zero_()
-        self.d_backward(PD, None, D["ones"], alpha, gimg=D["gimg"])     # d(sum D)/dx
-        ops.gp_penalty(D["gimg"], self.hyper.W_gp, self.loss[2:3], D["gp_norms"], D["gbar"])
-        tout, inj = self.d_tangent(PD, GD, D["gbar"], D["ones"], alpha)
+        if self._fused_penalty():
+            torch.sub(D["ones"].view(-1, 1), D["gp_eps"], out=D["gp_c"])
+            interp = L.ImgMix(xr, xf, D["gp_eps"], D["gp_c"])
+        else:
+            ops.gp_interp(xr, xf, D["gp_eps"], D["interp"])
+            interp = D["interp"]
+        self.d_forward(PD, interp, alpha)
+        gbar = self._input_grad(PD, D["ones"], alpha, "wgan-gp", self.hyper.W_gp)  # d(sum D)/dx
+        tout, inj = self.d_tangent(PD, GD, gbar, D["ones"], alpha)
         # upstream of the second backward: no BCE here, so no logit injection
-        self.d_backward(PD, GD, D["zeros"], alpha, img=D["interp"], inj_mbstd=inj, final=True)
+        self.d_backward(PD, GD, D["zeros"], alpha, img=interp, inj_mbstd=inj, final=True)
 
     def g_step(self, PG, PD, GG, z, alpha_G, alpha_D, before_d=None):
         """G half of train_step (pggan/model.py:244-253).  before_d() runs after the
@@ -995,8 +1040,11 @@ class StepEngine:
             before_d()
         self.d_forward(PD, img, alpha_D)
         ops.bce(D["logit"], True, hp.W_adv, self.loss[3:4], D["u"], None)   # pggan/loss.py:5-14
-        D["gimg"].zero_()
-        self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
+        if self._fused_penalty():
+            self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"], gimg_overwrite=True)
+        else:
+            D["gimg"].zero_()
+            self.d_backward(PD, None, D["u"], alpha_D, gimg=D["gimg"])
         self.g_backward(PG, GG, D["gimg"], alpha_G)
         self._side_join()
         return img

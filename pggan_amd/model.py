@@ -279,9 +279,12 @@ class ProgressiveGAN:
             eng.flush()
 
     # one training step captured once per (stage, schedule scalars) and replayed as a
-    # hipGraph (world == 1): the host enqueue of ~600 launches becomes one graph launch.
-    # PG_GRAPH=0 keeps every step eager.
-    use_graph = os.environ.get("PG_GRAPH", "1") != "0"
+    # hipGraph (world == 1, PG_GRAPH=1): the host enqueue of ~600 launches (6.3 ms) becomes
+    # one graph launch (1.5-1.7 ms).  Off by default: on ROCm 7.2 the replay of this
+    # two-stream step runs 6-7 % slower on the GPU than the eager streams (13.5 vs 12.55
+    # ms/step, interleaved A/B in one call, profiles/r3_graph_ab.txt), and the step is
+    # GPU-bound (12.5 ms of kernels vs 6.3 ms of host enqueue).
+    use_graph = os.environ.get("PG_GRAPH", "0") == "1"
     graph_replays = 0
 
     def _graph_key(self, eng, B):

@@ -224,6 +224,8 @@ class CpuOps:
             dbp.add_(fp * gs.reshape(-1, 3).sum(0))
 
     def _img_in(self, img, down):
+        if hasattr(img, "materialize"):      # pggan_amd._lib.ImgMix
+            img = img.materialize()
         iv = F.avg_pool2d(img, 2) if down else img
         return iv.permute(0, 2, 3, 1)
 
@@ -238,13 +240,19 @@ class CpuOps:
             a = F.leaky_relu(a, slope)
         y[..., :C] = a
 
-    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None):
+    def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None,
+                     gimg_overwrite=False, norms=None):
         g = gz[..., :C]
         if gimg is not None:
             gi = (c * g @ w.view(C, 3)).permute(0, 3, 1, 2)
             if down:
                 gi = up2(gi) * 0.25
-            gimg += gi
+            if gimg_overwrite:
+                gimg.copy_(gi)
+            else:
+                gimg += gi
+            if norms is not None:
+                norms += (gimg * gimg).reshape(gimg.shape[0], -1).sum(1)
         if dw is not None or db is not None:
             iv = self._img_in(img, down)
             if dw is not None:
@@ -352,6 +360,19 @@ class CpuOps:
         lv = logits.reshape(-1)
         loss += w * (lv * lv).sum()
         u += 2 * w * lv
+
+    def penalty_scale(self, mode, norms, w, loss, scale):
+        B = norms.numel()
+        if mode == "r1":
+            loss += 0.5 * norms.sum() / B
+            scale.fill_(1.0 / B)
+            norms.zero_()
+            return
+        else:
+            n = norms.sqrt()
+            loss += w * ((n - 1) ** 2).sum()
+            scale.copy_(torch.where(n > 0, w * 2 * (n - 1) / n, torch.zeros_like(n)))
+        norms.zero_()
 
     def r1_penalty(self, g, B, r1, gbar):
         r1 += 0.5 * (g * g).sum() / B

@@ -127,6 +127,8 @@ def run_step(eng, fpG, fpD, real, z1, z2, alpha, gp_eps=None, oracle_dtype=torch
     PD0 = {k: v.detach().cpu().clone() for k, v in fpD.views.items()}
     optG = _adam_state(fpG, hp.lr_G, hp, oracle_dtype)
     optD = _adam_state(fpD, hp.lr_D, hp, oracle_dtype)
+    optG2 = _adam_state(fpG, hp.lr_G, hp, oracle_dtype)   # for the Adam step on OUR gradients
+    optD2 = _adam_state(fpD, hp.lr_D, hp, oracle_dtype)
     rec = Recorder()
     eng.trace = rec
     try:
@@ -162,6 +164,15 @@ def run_step(eng, fpG, fpD, real, z1, z2, alpha, gp_eps=None, oracle_dtype=torch
     ref = dict(img_real=out.img_real, img_fake_D=out.img_fake_D, img_fake_G=out.img_fake_G,
                L_real=out.L_D_real, L_fake=out.L_D_fake, reg=out.R1, L_G=out.L_G,
                drift=out.drift, grads_D=out.grads_D, grads_G=out.grads_G, PD=PDr, PG=PGr)
+    # the oracle's Adam applied to OUR gradients (live parameters as the reference has them):
+    # with beta1 = 0 the first update is ~lr * g / (|g| + eps), so a near-zero gradient
+    # element that agrees with the oracle's to the gradient bar can still move its parameter
+    # by a visible fraction of lr; the Adam arithmetic itself is checked against this
+    for P0, opt, key, grads in ((PG0, optG2, "PG", out.grads_G), (PD0, optD2, "PD", out.grads_D)):
+        Pa = {k: cast(v) for k, v in P0.items()}
+        opt.update(Pa, {k: (None if g is None else cast(ours["grads_" + key[1]][k]))
+                        for k, g in grads.items()})
+        ref[key + "_adam_ours"] = Pa
     return ours, ref, rec.seq
 
 
@@ -200,9 +211,15 @@ def compare(ours, ref, fpG, fpD, kinks, *, tol, flip_bound, ptol=None, what=""):
                 continue
             errs[f"{net}:{n}"] = rel_l2(ours[key][n], g)
     if ptol is not None:
+        # parameters after Adam: within ptol of the oracle's step, or (a near-zero gradient
+        # element, see run_step) within ptol of the oracle's Adam on our gradients, which are
+        # themselves held to tol above
         for net, fp, key in (("D", fpD, "PD"), ("G", fpG, "PG")):
             for n in fp.names:
-                errs[f"param {net}:{n}"] = rel_l2(ours[key][n], ref[key][n])
+                e = rel_l2(ours[key][n], ref[key][n])
+                if e > ptol and key + "_adam_ours" in ref:
+                    e = min(e, rel_l2(ours[key][n], ref[key + "_adam_ours"][n]))
+                errs[f"param {net}:{n}"] = e
     bad = {k: v for k, v in errs.items()
            if v > (ptol if k.startswith("param") else tol) or not math.isfinite(v)}
     rep["errs"] = errs

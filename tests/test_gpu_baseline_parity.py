@@ -97,6 +97,30 @@ def test_fp32_step_matches_oracle_at_baseline_config(name, s, B, alpha, steps):
 
 
 @pytest.mark.timeout(900)
+def test_fp32_wgan_gp_step_matches_oracle_at_c2():
+    """C2 in the mode BASELINE.json names for it ("WGAN-GP on"): 128^2, B=16, alpha 1, the
+    optional WGAN-GP loss (pggan/loss.py:54-100: BCE + W_gp * sum_b (|grad D(x_hat_b)| - 1)^2
+    + W_drift_D * sum pred_real^2, configs.yaml:31-32), the interpolation / per-sample norm
+    and its double-backward on the HIP kernels; every tensor at the strict fp32 bar."""
+    from pggan_amd import engine as E
+    s, B, alpha = 5, 16, 1.0
+    eng, fpG, fpD = build(s, B, torch.float32, seed=705)
+    eng.hyper = E.Hyper(gp_mode="wgan-gp", W_gp=10.0, W_drift=0.001)
+    eng.bind(fpG, fpD, eng.hyper)
+    st = make_inputs(B, 4 * 2 ** s, seed=805, n_steps=1)[0]
+    real, z1, z2, eps = (torch.from_numpy(st[k]) for k in ("real", "z1", "z2", "gp_eps"))
+    ours, ref, kinks = K.run_step(eng, fpG, fpD, real, z1, z2, alpha, gp_eps=eps, threads=THREADS)
+    rep = K.compare(ours, ref, fpG, fpD, kinks, tol=1e-3, flip_bound=K.FLIP_BOUND[torch.float32],
+                    ptol=1e-5, what="C2 WGAN-GP: ")
+    assert ours["reg"] > 0.0 and ours["drift"] > 0.0
+    msg = K.summarize(rep)
+    print(f"\nC2 WGAN-GP fp32: {msg}", flush=True)
+    _report("C2_wgangp_fp32", rep, dict(config="C2", stage=s, batch=B, alpha=alpha, mode="f32",
+                                        loss="wgan-gp", oracle="float64 + injected kinks",
+                                        tol=1e-3, summary=msg))
+
+
+@pytest.mark.timeout(900)
 def test_bf16_bench_path_matches_oracle_at_c5():
     """The benchmarked configuration itself (bench.py: 1024^2, B=4, alpha 1, bf16)."""
     s, B, alpha = 8, 4, 1.0

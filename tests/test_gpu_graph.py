@@ -21,7 +21,7 @@ def build(args, graph, s):
     ProgressiveGAN.ops_factory = None
     torch.manual_seed(7)
     m = ProgressiveGAN(args, 0)
-    m.use_graph = graph
+    m.use_graph = graph         # (opt-in in the product: PG_GRAPH=1)
     m.initialize_models()
     for i in range(1, s + 1):
         m.G.add_block(args.depths[i])
