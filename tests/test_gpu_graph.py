@@ -43,7 +43,7 @@ def state(m):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_graph_replay_bitwise_equals_eager(tmp_path, dtype):
+def test_graph_replay_matches_eager(tmp_path, dtype):
     args = make_args(tmp_path, depths=list(TINY_DEPTHS), compute_dtype=dtype)
     s = 3
     eager, graph = build(args, False, s), build(args, True, s)
