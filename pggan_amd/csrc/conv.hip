@@ -1156,6 +1156,35 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t
     atomicAdd(dst, s * scale);
 }
 
+// The same sum, thread = 4 consecutive outputs: one 16-byte load per slab, RSP of them issued
+// before any is summed (the 4-byte form above kept 4 loads in flight per thread, ~9 KiB per CU:
+// latency bound at 1.2 TB/s).  Slabs are still summed in slab order into one register per
+// output, then added once to dw / db: the result is bitwise the form above's (gridDim.y == 1).
+// slab % 4 == 0 and nw % 4 == 0 (cout, cin multiples of 8), so a vector never straddles dw / db.
+constexpr int RSP = 16;
+__global__ __launch_bounds__(64) void wgrad_slab_reduce4(const float* ws, size_t slab, int splits,
+                                                         int nw, float* dw, float* db, float scale) {
+  const size_t i = ((size_t)blockIdx.x * 64 + threadIdx.x) * 4;
+  if (i >= slab) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < splits; k += RSP) {
+    f32x4_t t[RSP];
+#pragma unroll
+    for (int u = 0; u < RSP; ++u)
+      if (k + u < splits) t[u] = *reinterpret_cast<const f32x4_t*>(ws + (size_t)(k + u) * slab + i);
+#pragma unroll
+    for (int u = 0; u < RSP; ++u)
+      if (k + u < splits) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += t[u][e];
+      }
+  }
+  float* dst = i < (size_t)nw ? dw + i : (db ? db + (i - nw) : nullptr);
+  if (!dst) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) dst[e] += s[e] * scale;
+}
+
 struct WgbPlan {
   int MO, NC, WMO, WNC, BP;
   int ot, ct, splits, tiles_per_split, ntiles;
@@ -1273,7 +1302,14 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
-  if (p.mode == WG_SLABS) {
+  static const int red4 = getenv("PG_WG_RED4") ? atoi(getenv("PG_WG_RED4")) : 1;   // A/B switch
+  if (p.mode == WG_SLABS && red4 && pl.slab >= 65536 && pl.slab % 4 == 0 &&
+      ((uintptr_t)ws & 15) == 0) {
+    // wide layers (>= 256 blocks of 64 threads): vector form, one thread sums every split
+    hipLaunchKernelGGL(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
+                       (const float*)ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
+    PG_LAUNCH_CHECK();
+  } else if (p.mode == WG_SLABS) {
     const int nblk = (int)pg_cdiv((long long)pl.slab, 256);
     int ry = pg_cdiv(512, nblk);
     if (ry > pl.splits) ry = pl.splits;
