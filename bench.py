@@ -19,6 +19,14 @@ import os
 import sys
 import time
 
+# One process per GPU with the DP gradient exchange: RCCL's stream and the engine's two
+# streams must not share a hardware queue (HIP's default is 4 per process): a collective's
+# wait-on-event barrier in a shared queue stalls the compute kernels queued behind it
+# (bench.py --dp-exchange at one rank: -16 % of the step with 4 queues, -4 % with 8 or 16,
+# profiles/r3_dp_queues.txt).  Must be set before the HIP runtime starts.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dp-exchange" in sys.argv:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import torch
 import torch.distributed as dist
 
@@ -50,6 +58,9 @@ def parse():
                    help="0: the process's CPU share (OMP_NUM_THREADS, else os.cpu_count())")
     p.add_argument("--gp-mode", choices=["r1", "wgan-gp"], default="r1")
     p.add_argument("--no-kernel-events", action="store_true")
+    p.add_argument("--dp-exchange", action="store_true",
+                   help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
+                        "group), to measure the bookkeeping's cost against the plain step")
     return p.parse_args()
 
 
@@ -265,7 +276,8 @@ def build_model(args, rank, local, world, ops_factory):
     cfg = Config.from_yaml(os.path.join(ROOT, "pggan_amd", "default_config.yaml"))
     cfg.update(depths=list(PAPER_DEPTHS), batch_per_gpu=args.batch, compute_dtype=args.dtype,
                synthetic_data=True, isMaster=False, use_mGPU=world > 1, gpu_num=world,
-               run_id="bench", gp_mode=args.gp_mode)
+               run_id="bench", gp_mode=args.gp_mode,
+               dp_exchange_world1=bool(args.dp_exchange and world == 1))
     ProgressiveGAN.ops_factory = ops_factory
     torch.manual_seed(1234)                      # same init on every rank (then broadcast)
     m = ProgressiveGAN(cfg, local)
@@ -275,7 +287,7 @@ def build_model(args, rank, local, world, ops_factory):
         m.D.add_block(PAPER_DEPTHS[i])
     m.scale_index = args.stage
     m.G.alpha = m.D.alpha = args.alpha
-    if world > 1:
+    if world > 1 or args.dp_exchange:
         m.set_multi_GPU()                        # RCCL, parameter broadcast, GradExchange
     m.set_optimizers()
     m.set_dataset()
@@ -303,6 +315,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    elif args.dp_exchange:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        dist.init_process_group("nccl", device_id=dev, rank=0, world_size=1)
 
     from pggan_amd import _lib
 
@@ -477,8 +493,15 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        ex = getattr(model, "_exchange", None)
+        if ex is not None:
+            line["dp_exchange"] = dict(
+                note="world-1 RCCL group: grad_ready buckets + side-stream joins on"
+                if world == 1 else "RCCL", bucket_mb=ex.bucket_bytes / (1 << 20),
+                collectives_per_step=round(ex.calls / (args.warmup + args.steps + 3), 1),
+                host_ms_per_collective=round(1e3 * ex.host_s / max(ex.calls, 1), 3))
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -21,6 +21,8 @@ trade, the default fp32 keeps the DP contract exact to fp32 rounding).
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -36,7 +38,8 @@ class Pending:
             w.wait()
         for lo, hi, buf in self.casts:
             self.grad[lo:hi].copy_(buf)
-        self.grad.mul_(1.0 / self.world)
+        if self.world > 1:
+            self.grad.mul_(1.0 / self.world)
 
 
 class GradExchange:
@@ -51,6 +54,8 @@ class GradExchange:
         self.group = group
         self._fp = {}
         self._state = {}
+        self.calls = 0          # collectives launched, and the host seconds spent in them
+        self.host_s = 0.0
 
     def bind(self, net, fp):
         """fp: the net's engine.FlatParams (live parameters first)."""
@@ -58,6 +63,7 @@ class GradExchange:
         self._state[net] = dict(works=[], casts=[], pend=[], pend_elems=0, sent=[])
 
     def _launch(self, net, lo, hi):
+        t0 = time.perf_counter()
         st, g = self._state[net], self._fp[net].grad
         st["sent"].append((lo, hi))
         if self.reduce_dtype == torch.float32:
@@ -66,6 +72,8 @@ class GradExchange:
             buf = g[lo:hi].to(self.reduce_dtype)
             st["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
             st["casts"].append((lo, hi, buf))
+        self.calls += 1
+        self.host_s += time.perf_counter() - t0
 
     def _launch_merged(self, net, ranges):
         """One collective per maximal contiguous span of `ranges`."""

@@ -133,11 +133,18 @@ class ProgressiveGAN:
                                                                   self.args.gpu_num)))
         self.world, self.rank = dist.get_world_size(), dist.get_rank()
         self._broadcast_params()
-        if self.world > 1:
+        # dp_exchange_world1: the exchange also at one rank (an RCCL all-reduce over one
+        # rank), to measure what the DP bookkeeping costs the step (bench.py --dp-exchange)
+        if self.world > 1 or cfg_get(self.args, "dp_exchange_world1", False):
             from .dp import GradExchange
             rd = torch.bfloat16 if cfg_get(self.args, "dp_reduce_dtype", "f32") == "bf16" \
                 else torch.float32
-            self._exchange = GradExchange(self.world, reduce_dtype=rd)
+            # bucket size: PG_DP_BUCKET_MB (tuning) > config dp_bucket_mb > 32 MiB.  Each
+            # collective costs ~50-100 us of host time (torch + RCCL enqueue); 4 MiB buckets
+            # made the host enqueue the step's bound (bench.py --dp-exchange)
+            mb = float(os.environ.get("PG_DP_BUCKET_MB", cfg_get(self.args, "dp_bucket_mb", 32)))
+            self._exchange = GradExchange(self.world, bucket_bytes=int(mb * (1 << 20)),
+                                          reduce_dtype=rd)
 
     def _broadcast_params(self):
         if self.world > 1:

@@ -10,6 +10,14 @@ all-reduced over RCCL).
 import os
 import sys
 
+# One process per GPU with the DP gradient exchange: RCCL's stream and the engine's two
+# streams must not share a hardware queue (HIP's default is 4 per process): a collective's
+# wait-on-event barrier in a shared queue stalls the compute kernels queued behind it
+# (bench.py --dp-exchange at one rank: -16 % of the step with 4 queues, -4 % with 8 or 16,
+# profiles/r3_dp_queues.txt).  Must be set before the HIP runtime starts.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dp-exchange" in sys.argv:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
