@@ -37,6 +37,11 @@ class Pending:
         for w in self.works:
             w.wait()
         for lo, hi, buf in self.casts:
+            # buf was allocated on the stream that launched the collective (the weight-gradient
+            # stream): tell the caching allocator this stream reads it too, or the block could be
+            # handed out again there before this copy has run
+            if buf.is_cuda:
+                buf.record_stream(torch.cuda.current_stream(buf.device))
             self.grad[lo:hi].copy_(buf)
         if self.world > 1:
             self.grad.mul_(1.0 / self.world)

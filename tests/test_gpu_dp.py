@@ -31,7 +31,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, reduce_bf16=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.dirname(here), here, os.path.join(here, "golden")):
@@ -54,7 +54,8 @@ def _worker(rank, world, port, out_dir):
     fpD = E.FlatParams(dsh, E.dead_params("D", S), "cuda", PD)
     eng = E.StepEngine(_lib.HipOps(torch.float32), TINY_DEPTHS, S, B, "cuda")
     eng.bind(fpG, fpD, E.Hyper())
-    ex = GradExchange(world, bucket_bytes=64 << 10)   # small buckets: several per net
+    ex = GradExchange(world, bucket_bytes=64 << 10,   # small buckets: several per net
+                      reduce_dtype=torch.bfloat16 if reduce_bf16 else torch.float32)
     ex.bind("G", fpG)
     ex.bind("D", fpD)
     eng.grad_ready = ex.ready
@@ -82,9 +83,13 @@ def _worker(rank, world, port, out_dir):
 
 
 @pytest.mark.timeout(300)
-def test_dp_two_ranks_on_hip_kernels(tmp_path):
+@pytest.mark.parametrize("reduce", ["f32", "bf16"])
+def test_dp_two_ranks_on_hip_kernels(tmp_path, reduce):
+    """reduce = bf16 (dp_reduce_dtype): each rank's gradient is rounded to bf16 before the
+    sum, so the mean is held to 1e-2 relative L2 (2^-8 rounding per addend) instead of 1e-3."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), reduce == "bf16"), nprocs=world,
+             join=True)
     r = [np.load(tmp_path / f"rank{i}.npz") for i in range(world)]
     for k in ("gD", "gG", "pD", "pG"):
         assert np.array_equal(r[0][k], r[1][k]), f"{k} differs across ranks"
@@ -98,4 +103,4 @@ def test_dp_two_ranks_on_hip_kernels(tmp_path):
         lo, hi = fpD.offsets[n], fpD.offsets[n] + int(np.prod(fpD.shapes[n]))
         a, b = r[0]["gD"][lo:hi].astype(np.float64), ref[lo:hi]
         err = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
-        assert err <= 1e-3, (n, err)
+        assert err <= (1e-2 if reduce == "bf16" else 1e-3), (n, err)
