@@ -49,6 +49,7 @@ struct ConvParams {
   int lg_tx, lg_ty;   // conv_hr: log2 of the tile counts along x and y
   int xcd_remap;      // conv3x3_kernel: XCD-aware workgroup order
   int diag;           // conv_hr: timing diagnostics (PG_HR_DIAG), 0 in every real launch
+  int tpw;            // conv_hr 8-wave LDS-DMA tile: tiles per workgroup (> 1: persistent form)
 };
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }

@@ -75,6 +75,12 @@ CONV_CASES = [
     (4, 128, 64, 128, ("bias", "lrelu")),
     (8, 128, 64, 64, ("ups", "bias", "lrelu", "pool")),
     (4, 128, 128, 128, ("mask", "accum")),
+    # tile 3's persistent form (more tiles than one round of workgroups): one chunk with the
+    # pre-pool copy staged in the same LDS slot as the pooled output, two chunks x two
+    # output-channel blocks, two chunks with bias
+    (4, 256, 32, 64, ("bias", "lrelu", "pool")),
+    (2, 256, 64, 128, ("mask", "accum")),
+    (4, 256, 64, 64, ("bias", "lrelu")),
 ]
 
 
