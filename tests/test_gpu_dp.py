@@ -86,7 +86,8 @@ def _worker(rank, world, port, out_dir, reduce_bf16=False):
 @pytest.mark.parametrize("reduce", ["f32", "bf16"])
 def test_dp_two_ranks_on_hip_kernels(tmp_path, reduce):
     """reduce = bf16 (dp_reduce_dtype): each rank's gradient is rounded to bf16 before the
-    sum, so the mean is held to 1e-2 relative L2 (2^-8 rounding per addend) instead of 1e-3."""
+    sum, so the mean is held to 1e-2 of the addends' L2 norm (2^-8 rounding per addend)
+    instead of 1e-3 of the result's."""
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), reduce == "bf16"), nprocs=world,
              join=True)
@@ -102,5 +103,12 @@ def test_dp_two_ranks_on_hip_kernels(tmp_path, reduce):
             continue
         lo, hi = fpD.offsets[n], fpD.offsets[n] + int(np.prod(fpD.shapes[n]))
         a, b = r[0]["gD"][lo:hi].astype(np.float64), ref[lo:hi]
-        err = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        if reduce == "bf16":
+            # the rounding is of each rank's addend (and of the bf16 sum): measured against the
+            # addends' magnitude, since a mean of opposite-signed terms (a bias gradient) can
+            # cancel to far below them
+            scale = sum(np.abs(x["gD_ref"][lo:hi]) for x in r) / world
+            err = np.linalg.norm(a - b) / max(np.linalg.norm(scale), 1e-30)
+        else:
+            err = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
         assert err <= (1e-2 if reduce == "bf16" else 1e-3), (n, err)
