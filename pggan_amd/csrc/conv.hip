@@ -1245,6 +1245,34 @@ size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
   return pl.splits > 1 ? pl.splits * pl.slab * sizeof(float) : 0;
 }
 
+// The second launch of the WG_SLABS mode: the split partials summed into dw / db
+int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const float* ws, float* dw,
+                      float* db, float scale, hipStream_t st) {
+  if (mode != WG_SLABS) return PG_OK;
+  static const int red4 = getenv("PG_WG_RED4") ? atoi(getenv("PG_WG_RED4")) : 1;   // A/B switch
+  if (red4 && pl.slab >= 65536 && pl.slab % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
+    // wide layers (>= 256 blocks of 64 threads): vector form, one thread sums every split
+    hipLaunchKernelGGL(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
+                       ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
+  const int nblk = (int)pg_cdiv((long long)pl.slab, 256);
+  int ry = pg_cdiv(512, nblk);
+  if (ry > pl.splits) ry = pl.splits;
+  const int spb = pg_cdiv(pl.splits, ry);
+  ry = pg_cdiv(pl.splits, spb);
+  hipLaunchKernelGGL(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, ws, pl.slab, pl.splits, spb,
+                     d->cout * d->cin * 9, dw, db, scale);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
+// the LDS-DMA weight gradient of the wide layers (wgrad_dma.inc)
+bool wgrad_dma_ok(const pg_conv_desc* d, const WgbPlan& pl);
+int launch_wgrad_dma(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz, float scale,
+                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st);
+
 template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false, int BP = WGB_BP>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
                       float scale, float* dw, float* db, float* ws, size_t ws_bytes,
@@ -1303,24 +1331,7 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
-  static const int red4 = getenv("PG_WG_RED4") ? atoi(getenv("PG_WG_RED4")) : 1;   // A/B switch
-  if (p.mode == WG_SLABS && red4 && pl.slab >= 65536 && pl.slab % 4 == 0 &&
-      ((uintptr_t)ws & 15) == 0) {
-    // wide layers (>= 256 blocks of 64 threads): vector form, one thread sums every split
-    hipLaunchKernelGGL(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
-                       (const float*)ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
-    PG_LAUNCH_CHECK();
-  } else if (p.mode == WG_SLABS) {
-    const int nblk = (int)pg_cdiv((long long)pl.slab, 256);
-    int ry = pg_cdiv(512, nblk);
-    if (ry > pl.splits) ry = pl.splits;
-    const int spb = pg_cdiv(pl.splits, ry);
-    ry = pg_cdiv(pl.splits, spb);
-    hipLaunchKernelGGL(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, (const float*)ws,
-                       pl.slab, pl.splits, spb, d->cout * d->cin * 9, dw, db, scale);
-    PG_LAUNCH_CHECK();
-  }
-  return PG_OK;
+  return wgrad_slab_finish(d, pl, p.mode, ws, dw, db, scale, st);
 }
 
 // GZ_BITS variants: the tiles of the discriminator's conv b weight gradient at the levels
@@ -1337,6 +1348,7 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
   const WgbPlan pl = wgrad_bf16_plan(d);
+  if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
   // (prefetch depth, waves per SIMD); PG_WG_VARIANT="pd,wpe" overrides for tuning runs
   int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   if (const char* e = getenv("PG_WG_VARIANT")) sscanf(e, "%d,%d", &pd, &wpe);
@@ -1621,6 +1633,7 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 
 #include "conv_hr.inc"
 #include "conv_lr.inc"
+#include "wgrad_dma.inc"
 
 // Which fused epilogues the kernel the dispatcher picks supports.
 template <typename T>

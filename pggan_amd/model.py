@@ -357,15 +357,6 @@ class ProgressiveGAN:
         self.graph_replays += 1
         return gs["out"]
 
-    def _main_stream(self):
-        """PG_MAIN_PRIO=1: a high-priority stream for the step's main launches (A/B)."""
-        if os.environ.get("PG_MAIN_PRIO", "0") != "1" or self.device.type != "cuda":
-            return None
-        if getattr(self, "_ms", None) is None:
-            lo, hi = torch.cuda.Stream.priority_range()
-            self._ms = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
-        return self._ms
-
     def train_step(self):
         """pggan/model.py:206-255; returns [img_real, img_fake]."""
         img_real = self.load_next_batch()
@@ -389,18 +380,7 @@ class ProgressiveGAN:
         if out is None:
             if key is None:        # an eager step may change what a captured graph assumed
                 self.__dict__.pop("_gstate", None)
-            ms = self._main_stream()
-            if ms is None:
-                out = self._step_body(eng, img_real, B)
-            else:
-                # the step's critical path (the input-gradient chain) on a high-priority
-                # stream: where its kernels and the weight-gradient stream's are both ready,
-                # the dispatcher serves the chain first
-                cur = torch.cuda.current_stream(self.device)
-                ms.wait_stream(cur)
-                with torch.cuda.stream(ms):
-                    out = self._step_body(eng, img_real, B)
-                cur.wait_stream(ms)
+            out = self._step_body(eng, img_real, B)
         img_real, _, img_fake = out
         self.loss_collector.attach(eng.loss, self.hyper.gp_mode)
         return [img_real, img_fake]

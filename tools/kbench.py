@@ -59,9 +59,14 @@ def run(ops, spec, B, iters):
         dw = torch.zeros(cout, cin, 3, 3, device=dev)
         db = torch.zeros(cout, device=dev)
 
+        # the split-partial workspace the engine passes (WG_SLABS + the reduction launch);
+        # without one the kernel would fall back to fp32 atomics
+        nbw = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=bool(fl))
+        wsw = torch.empty(max(nbw // 4, 1), device=dev) if nbw else None
+
         def f():
             ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=bool(fl), scale=1.0,
-                           db=db)
+                           db=db, ws=wsw)
         byts = x.numel() * 2 + gz.numel() * 2
     for _ in range(3):
         f()
