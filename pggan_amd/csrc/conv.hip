@@ -1202,7 +1202,12 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // two 16-channel halves of a 32-channel input slice per workgroup (waves split the
   // channels, the gz tile is staged once for both): A/B -5..-22 % at 32^2-256^2 for
   // cin > 32; below 32^2 the single-half tile is faster
-  pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32) ? 2 : 1;
+  // the 16^2 wide layers: two halves too when wgrad_dma_kernel takes them (it needs WNC = 2;
+  // PG_WG_DMA16=0 keeps the register-staged single-half tile, A/B)
+  static const int dma16 = getenv("PG_WG_DMA16") ? atoi(getenv("PG_WG_DMA16")) : 1;
+  const bool w16_dma = dma16 && d->W == 16 && d->H % 8 == 0 && co % 64 == 0 && ci % 32 == 0 &&
+                       !(d->flags & PG_CONV_GZ_BITS);
+  pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32 || w16_dma) ? 2 : 1;
   // ... unless the single-half tiles overflow one round of workgroups (the 513-channel
   // minibatch-stddev conv at 4^2: 8 x 33 = 264 > 256 ran as two rounds, 29.6 us vs 15.8)
   if (pl.WNC == 1 && ci > 16 && pg_cdiv(co, co <= 16 ? 16 : co <= 32 ? 32 : 64) * pg_cdiv(ci, 16) > 256)

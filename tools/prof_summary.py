@@ -6,7 +6,7 @@
 
 Families (same bracketing as bench.py's HIP events):
   conv3x3  = conv3x3_kernel dispatches + their split-K epilogue dispatches, per conv call
-  wgrad3x3 = wgrad3x3_kernel / wgrad_bf16_kernel dispatches (bias grad fused), per call
+  wgrad3x3 = wgrad3x3_kernel / wgrad_bf16_kernel / wgrad_dma_kernel dispatches (bias grad fused), per call
 Traffic per call = 2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md "HBM [CDNA4]": gfx950
 FETCH_SIZE reports half of the bytes of wide coalesced reads; WRITE_SIZE is exact for
 16-B stores and float atomics), summed over the family's dispatches / calls.
@@ -24,7 +24,7 @@ def family(name):
         return "conv3x3", True
     if "conv_splitk_epilogue" in name:
         return "conv3x3", False
-    if "wgrad3x3_kernel" in name or "wgrad_bf16_kernel" in name:
+    if "wgrad3x3_kernel" in name or "wgrad_bf16_kernel" in name or "wgrad_dma_kernel" in name:
         return "wgrad3x3", True
     if "wgrad_slab_reduce" in name:
         return "wgrad3x3", False
