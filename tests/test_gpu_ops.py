@@ -147,7 +147,9 @@ WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, Fa
                (1, 64, 8, 8, False), (2, 32, 64, 32, True),
                # bench-like: many pixel splits (slabs), direct single split, ups + cin 32
                (4, 128, 16, 32, False), (4, 32, 512, 512, False), (2, 64, 32, 16, True),
-               (4, 64, 64, 128, False)]
+               (4, 64, 64, 128, False),
+               # the LDS-DMA kernel at 16^2 (one 16-wide tile per row) and with the upsample
+               (4, 16, 512, 512, False), (2, 64, 256, 128, True)]
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
