@@ -1193,6 +1193,8 @@ struct WgbPlan {
   size_t slab;
 };
 
+bool wgrad_dma_ok(const pg_conv_desc* d, const WgbPlan& pl);
+
 WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   WgbPlan pl;
   const int co = d->cout, ci = d->cin;
@@ -1233,6 +1235,16 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // (tools/wg_target_sweep.sh: 512 for the narrow tiles, 80.9 -> 59.2 us at 512^2 32->32,
   // 86 -> 79 at 1024^2 16->16, 108 -> 99 at 1024^2 16->32: half the slab traffic)
   int target = pl.MO >= 4 ? 256 : 512;
+  // the LDS-DMA narrow tiles (tools/wg_target_dma.sh): (2,2) at 512^2 in one round of
+  // workgroups (8 waves at 164 VGPRs: one workgroup per CU), 51.0 -> 48.8 us at 32->32;
+  // (1,1) at 1024^2 with ~4 per CU, 74.3 -> 62.7 us at 16->16
+  if (pl.MO < 4) {
+    pl.tiles_per_split = 1;
+    if (wgrad_dma_ok(d, pl)) {
+      if (pl.MO == 2 && pl.WNC == 2) target = 256;
+      else if (pl.MO == 1 && pl.WNC == 1) target = 1024;
+    }
+  }
   if (const char* e = getenv("PG_WG_TARGET")) target = atoi(e);   // tuning runs only
   if (const char* e = getenv("PG_WG_TARGET_NARROW")) { if (pl.MO < 4) target = atoi(e); }   // A/B
   int splits = base >= 256 ? 1 : pg_cdiv(target, base);
@@ -1276,7 +1288,7 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
 // the LDS-DMA weight gradient of the wide layers (wgrad_dma.inc)
 bool wgrad_dma_ok(const pg_conv_desc* d, const WgbPlan& pl);
 int launch_wgrad_dma(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz, float scale,
-                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st);
+                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st, const void* gzbits);
 
 template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false, int BP = WGB_BP>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
@@ -1353,7 +1365,7 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
   const WgbPlan pl = wgrad_bf16_plan(d);
-  if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st);
+  if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits);
   // (prefetch depth, waves per SIMD); PG_WG_VARIANT="pd,wpe" overrides for tuning runs
   int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   if (const char* e = getenv("PG_WG_VARIANT")) sscanf(e, "%d,%d", &pd, &wpe);

@@ -53,21 +53,27 @@ def run(ops, spec, B, iters):
                         aux=aux, ws=ws, out_scale=0.25 if fl & 16 else 1.0, y2=y2, xbits=xbits)
         byts = sum(t.numel() * t.element_size() for t in (x, y, aux, y2, xbits) if t is not None)
     else:
-        Hin = H // 2 if fl else H
+        # w flags: 1 = UPS_IN (x at half resolution), 2 = GZ_BITS (g at half resolution,
+        # masked by lrelu' sign bits at full resolution: the D conv-b weight gradient)
+        ups, gzb = bool(fl & 1), bool(fl & 2)
+        Hin = H // 2 if ups else H
         x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
-        gz = torch.randn(B, H, H, r8(cout), device=dev, generator=g).to(bf)
+        Hg = H // 2 if gzb else H
+        gz = torch.randn(B, Hg, Hg, r8(cout), device=dev, generator=g).to(bf)
+        bits = (torch.randint(0, 256, (B, H, H, r8(cout) // 8), device=dev, generator=g,
+                              dtype=torch.uint8) if gzb else None)
         dw = torch.zeros(cout, cin, 3, 3, device=dev)
         db = torch.zeros(cout, device=dev)
 
         # the split-partial workspace the engine passes (WG_SLABS + the reduction launch);
         # without one the kernel would fall back to fp32 atomics
-        nbw = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=bool(fl))
+        nbw = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=ups)
         wsw = torch.empty(max(nbw // 4, 1), device=dev) if nbw else None
 
         def f():
-            ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=bool(fl), scale=1.0,
-                           db=db, ws=wsw)
-        byts = x.numel() * 2 + gz.numel() * 2
+            ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=1.0,
+                           db=db, ws=wsw, gzbits=bits)
+        byts = x.numel() * 2 + gz.numel() * 2 + (bits.numel() if gzb else 0)
     for _ in range(3):
         f()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
