@@ -29,6 +29,22 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   v[1] = (__bf16)b;
   return __builtin_bit_cast(uint32_t, v);
 }
+// lrelu'-mask of 8 bf16 (one 16-B vector) by one sign-bit byte: element j keeps its value
+// when bit j is set, else becomes round(x * slope) -- branch-free: the factor (1.0 or slope)
+// is one bitfield insert from the bit sign-extended (x * 1.0 == x, so the kept elements
+// round-trip exactly and the result equals the per-element branch)
+__device__ __forceinline__ u32x4_t lrelu_mask_bf16x8(u32x4_t v, unsigned m, float slope) {
+  const unsigned one = __float_as_uint(1.0f), sl = __float_as_uint(slope);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned ka = (unsigned)(((int)(m << (31 - 2 * i))) >> 31);       // bit 2i -> 0 / ~0
+    const unsigned kc = (unsigned)(((int)(m << (30 - 2 * i))) >> 31);       // bit 2i+1
+    const float fa = __uint_as_float((ka & one) | (~ka & sl));
+    const float fc = __uint_as_float((kc & one) | (~kc & sl));
+    v[i] = pack_bf16x2(__uint_as_float(v[i] << 16) * fa, __uint_as_float(v[i] & 0xffff0000u) * fc);
+  }
+  return v;
+}
 __device__ __forceinline__ bf16_t f2bf(float f) {
   const __bf16 h = (__bf16)f;
   return __builtin_bit_cast(bf16_t, h);
