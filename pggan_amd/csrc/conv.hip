@@ -1247,6 +1247,7 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   }
   if (const char* e = getenv("PG_WG_TARGET")) target = atoi(e);   // tuning runs only
   if (const char* e = getenv("PG_WG_TARGET_NARROW")) { if (pl.MO < 4) target = atoi(e); }   // A/B
+  if (const char* e = getenv("PG_WG_TARGET_WIDE")) { if (pl.MO >= 4) target = atoi(e); }     // A/B
   int splits = base >= 256 ? 1 : pg_cdiv(target, base);
   const int max_splits = pl.ntiles / 2 > 1 ? pl.ntiles / 2 : 1;
   if (splits > max_splits) splits = max_splits;
