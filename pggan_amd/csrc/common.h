@@ -152,3 +152,24 @@ void pg_set_error(const char* fmt, ...);
   } while (0)
 
 static inline int pg_cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// Opt kernel `fn` (parenthesise template arguments) in to `bytes` of dynamic LDS on the
+// current device, once per (call site, device): the attribute is per device, and a failed set
+// is reported here with its reason instead of surfacing later as a bare launch error.
+#define PG_LDS_ATTR(fn, bytes)                                                               \
+  do {                                                                                       \
+    static unsigned done_ = 0;                                                               \
+    int dev_ = 0;                                                                            \
+    (void)hipGetDevice(&dev_);                                                               \
+    if (!((done_ >> (dev_ & 31)) & 1u)) {                                                    \
+      const hipError_t e_ = hipFuncSetAttribute((const void*)(fn),                           \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                                (int)(bytes));                               \
+      if (e_ != hipSuccess) {                                                                \
+        pg_set_error("%s: %d B of dynamic LDS: %s", __func__, (int)(bytes),                  \
+                     hipGetErrorString(e_));                                                 \
+        return PG_ERR_HIP;                                                                   \
+      }                                                                                      \
+      done_ |= 1u << (dev_ & 31);                                                            \
+    }                                                                                        \
+  } while (0)

@@ -1340,12 +1340,7 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
-  static bool attr_done = false;
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_done = true;
-  }
+  PG_LDS_ATTR((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), 160 * 1024);
   hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
@@ -1604,12 +1599,7 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.xcd_remap = xcd;
   dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
             splits);
-  static bool attr_done = false;
-  if (!attr_done) {
-    (void)hipFuncSetAttribute((const void*)conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_done = true;
-  }
+  PG_LDS_ATTR((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), 160 * 1024);
   hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(256), lds, st, p);
   if (splits > 1) {
     const bool pool = (d->flags & PG_CONV_POOL) != 0;

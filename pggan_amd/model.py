@@ -205,12 +205,14 @@ class ProgressiveGAN:
         self.train_dataset = ds
 
     def set_data_iterator(self):
-        """lib/model.py:44-52: one process reads the dataset in order (DataLoader without a
-        sampler, no shuffle); with DP each rank reads its DistributedSampler shard (seed 0,
-        set_epoch never called, so every epoch repeats the same order: SURVEY Appendix A.4)."""
+        """lib/model.py:44-52: without use_mGPU the dataset is read in order (DataLoader without
+        a sampler, no shuffle); with use_mGPU (any world size, one included) each rank reads its
+        DistributedSampler shard (seed 0, set_epoch never called, so every epoch repeats the
+        same order: SURVEY Appendix A.4)."""
         self._order, self._pos = None, 0
         if self.train_dataset is not None:
-            self._order = sampler_order(len(self.train_dataset), self.rank, self.world)
+            self._order = sampler_order(len(self.train_dataset), self.rank, self.world,
+                                        distributed=bool(cfg_get(self.args, "use_mGPU", False)))
 
     def load_next_batch(self):
         """pggan/model.py:104-115."""
@@ -336,6 +338,16 @@ class ProgressiveGAN:
         if gs.get("key") != key:
             gs.clear()
             gs["key"] = key          # first step with this key: eager (warms every lazy buffer)
+            return None
+        # the graph's kernels read the device-side Adam step counts and RNG offset and advance
+        # them, and a capture would record the host's re-sync of them (a fill) into the graph:
+        # capture or replay only while the host's counts are the ones the device holds.  An
+        # optimizer load_state_dict or a schedule reset changes a host count alone; that step
+        # runs eagerly (which rewrites the device copies) and the next one captures again.
+        if (any(fp._step_dev_host != fp.step for fp in (self.fpG, self.fpD)) or
+                getattr(self, "_rng_off_host", None) != self._rng_step * self._z.numel()):
+            gs.clear()
+            gs["key"] = key
             return None
         if "graph" not in gs:
             gs["real"] = img_real if img_real is self.synthetic else img_real.clone()
@@ -503,13 +515,16 @@ class ProgressiveGAN:
         Image.fromarray(np.clip(np.rint(grid), 0, 255).astype(np.uint8)).save(f"{d}/e{step}.jpg")
 
 
-def sampler_order(n, rank, world):
-    """The sample order rank `rank` of `world` reads (lib/model.py:50-51).  world == 1: the
-    reference builds its DataLoader without a sampler, i.e. in order.  world > 1:
-    torch.utils.data.DistributedSampler(dataset) with its defaults (shuffle, seed 0,
-    drop_last False) at epoch 0 -- torch.randperm(n) from a generator seeded with 0, padded
-    by wrapping to a multiple of world, then every world-th index from rank."""
-    if world <= 1:
+def sampler_order(n, rank, world, distributed=None):
+    """The sample order rank `rank` of `world` reads (lib/model.py:50-51).  The reference picks
+    the sampler from args.use_mGPU (`distributed`; None: world > 1).  Without it the DataLoader
+    has no sampler, i.e. in order.  With it: torch.utils.data.DistributedSampler(dataset) with
+    its defaults (shuffle, seed 0, drop_last False) at epoch 0 -- torch.randperm(n) from a
+    generator seeded with 0, padded by wrapping to a multiple of world, then every world-th
+    index from rank (world may be 1: the whole permutation)."""
+    if distributed is None:
+        distributed = world > 1
+    if not distributed:
         return np.arange(n)
     g = torch.Generator().manual_seed(0)
     idx = torch.randperm(n, generator=g).tolist()

@@ -57,6 +57,13 @@ def test_graph_replay_matches_eager(tmp_path, dtype):
             sd = {k: v.clone() * 1.01 for k, v in eager.G.state_dict().items()}
             for m in (eager, graph):
                 m.G.load_state_dict(sd)
+        if step == 7:           # optimizer state alone: the host Adam count changes, no
+            # parameter version does -- the replay must not run with the device's old count
+            for m in (eager, graph):
+                sd = m.opt_D.state_dict()
+                for st in sd["state"].values():
+                    st["step"] = torch.tensor(float(m.fpD.step - 2))
+                m.opt_D.load_state_dict(sd)
         eager.train_step()
         graph.train_step()
         torch.cuda.synchronize()

@@ -75,9 +75,9 @@ CONV_CASES = [
     (4, 128, 64, 128, ("bias", "lrelu")),
     (8, 128, 64, 64, ("ups", "bias", "lrelu", "pool")),
     (4, 128, 128, 128, ("mask", "accum")),
-    # tile 3's persistent form (more tiles than one round of workgroups): one chunk with the
-    # pre-pool copy staged in the same LDS slot as the pooled output, two chunks x two
-    # output-channel blocks, two chunks with bias
+    # tile 3 with more tiles than one round of workgroups (the default one-tile-per-workgroup
+    # launch; the opt-in persistent form, PG_HR_MT=1, is not run by this suite): one chunk
+    # with the pre-pool copy, two chunks x two output-channel blocks, two chunks with bias
     (4, 256, 32, 64, ("bias", "lrelu", "pool")),
     (2, 256, 64, 128, ("mask", "accum")),
     (4, 256, 64, 64, ("bias", "lrelu")),
@@ -148,7 +148,8 @@ WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, Fa
                # bench-like: many pixel splits (slabs), direct single split, ups + cin 32
                (4, 128, 16, 32, False), (4, 32, 512, 512, False), (2, 64, 32, 16, True),
                (4, 64, 64, 128, False),
-               # the LDS-DMA kernel at 16^2 (one 16-wide tile per row) and with the upsample
+               # the 16^2 wide layer (the register-staged kernel by default; the opt-in LDS-DMA
+               # form, PG_WG_DMA16=1, is not run by this suite) and the LDS-DMA kernel with ups
                (4, 16, 512, 512, False), (2, 64, 256, 128, True)]
 
 

@@ -56,3 +56,11 @@ def test_sampler_order_matches_distributed_sampler(n, world):
             want = np.asarray(list(iter(s)))
         assert np.array_equal(got, want), (rank, got[:8], want[:8])
         assert len(got) == (n if world == 1 else math.ceil(n / world))
+
+
+@pytest.mark.parametrize("n", [10, 7])
+def test_sampler_order_use_mgpu_one_rank(n):
+    """use_mGPU with gpu_num = 1: the reference still builds a DistributedSampler (shuffled)."""
+    s = torch.utils.data.distributed.DistributedSampler(list(range(n)), num_replicas=1, rank=0)
+    assert np.array_equal(sampler_order(n, 0, 1, distributed=True), np.asarray(list(iter(s))))
+    assert np.array_equal(sampler_order(n, 0, 1, distributed=False), np.arange(n))
