@@ -1643,6 +1643,13 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 #include "conv_lr.inc"
 #include "wgrad_dma.inc"
 
+}  // namespace
+// the K-grouped wide conv (conv_kg.hip)
+bool conv_kg_ok(const pg_conv_desc* d);
+int conv_kg_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias, const void* aux,
+                     void* y, void* y2, hipStream_t st);
+namespace {
+
 // Which fused epilogues the kernel the dispatcher picks supports.
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
@@ -1684,6 +1691,7 @@ int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const f
                d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
     if (conv_lr_ok(d)) return conv_lr_dispatch(d, x, wpk, bias, aux, y, y2, st);
+    if (conv_kg_ok(d)) return conv_kg_dispatch(d, x, wpk, bias, aux, y, y2, st);
     if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, xbits, st);
   }
   int BM, BN;
@@ -1894,7 +1902,8 @@ namespace {
 struct PlanLayer {
   char net, kind[8];
   int H, cin, cout, ups;
-  int fwd_path, dgrad_path;   // 0 conv3x3 (split-K when ws > 0), 1 conv_hr tile t, 2 conv_lr
+  int fwd_path, dgrad_path;   // 0 conv3x3 (split-K when ws > 0), 1 conv_hr tile t, 2 conv_lr,
+                              // 3 conv_kg
   int fwd_tile, dgrad_tile;
   size_t fwd_ws, dgrad_ws, wgrad_ws;
   int wg_MO, wg_WNC, wg_splits;
@@ -1915,6 +1924,7 @@ void plan_conv(int dtype, pg_conv_desc* d, int* path, int* tile, size_t* ws) {
   *tile = -1;
   if (dtype == PG_BF16) {
     if (conv_lr_ok(d)) { *path = 2; *ws = 0; return; }
+    if (conv_kg_ok(d)) { *path = 3; *ws = 0; return; }
     if (conv_hr_ok(d)) { *path = 1; *tile = conv_hr_tile(d); *ws = 0; }
   }
 }
@@ -1971,7 +1981,7 @@ size_t pg_step_plan_workspace_size(const pg_step_plan* plan) { return plan ? pla
 
 int pg_step_plan_describe(const pg_step_plan* plan, char* buf, size_t len) {
   PG_CHECK_ARG(plan && buf && len > 0, "step_plan_describe: bad arguments");
-  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr"};
+  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr", "conv_kg"};
   size_t o = 0;
   auto put = [&](const char* fmt, auto... a) {
     if (o < len) o += snprintf(buf + o, len - o, fmt, a...);

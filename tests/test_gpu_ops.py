@@ -421,6 +421,72 @@ def test_conv3x3_splitk(case, dtype):
         cmp(outs[0][1], outs[1][1], tol_for(dtype), "splitk y2")
 
 
+KG_CASES = [
+    # the K-grouped wide kernel (conv_kg.hip): 8-row tiles at 32^2 (3-slot ring), 16-row at
+    # 64^2, 32-row at >= 128^2; every epilogue it takes
+    (4, 32, 512, 512, ("bias", "lrelu")),
+    (4, 32, 512, 512, ("mask", "accum")),
+    (4, 32, 512, 512, ("bias", "lrelu", "pool")),
+    (4, 64, 256, 256, ()),
+    (4, 64, 256, 512, ("bias", "lrelu", "pool")),
+    (4, 64, 512, 256, ("ups", "bias", "lrelu")),
+    (4, 64, 256, 256, ("pool", "accum")),
+    (4, 128, 128, 128, ("mask",)),
+    (4, 128, 256, 128, ("ups", "bias", "lrelu")),
+    (2, 256, 64, 128, ("bias", "lrelu", "pool")),
+    (4, 256, 128, 64, ("ups", "bias", "lrelu", "pixnorm")),
+    (4, 256, 64, 64, ("bias", "lrelu", "pixnorm")),
+    (2, 256, 64, 64, ("mask", "accum")),
+    # one-slot form (two workgroups per CU): one- and two-chunk layers at >= 256^2
+    (4, 256, 64, 64, ("bias", "lrelu")),
+    (4, 256, 64, 128, ("mask",)),
+    (2, 512, 32, 64, ("bias", "lrelu", "pool")),
+    (2, 512, 32, 64, ()),
+]
+
+
+@pytest.mark.parametrize("case", KG_CASES)
+def test_conv_kg(case):
+    """bf16 wide convs through the K-grouped kernel against the CPU double: output, the
+    pre-pool copy (y2 with POOL) and the PixelNorm factor (y2 with PIXNORM)."""
+    B, H, cin, cout, fl = case
+    _L = lib()
+    dtype = torch.bfloat16
+    hip, cpu = ops_pair(dtype)
+    flags = 0
+    for f, v in (("ups", _L.CONV_UPS_IN), ("bias", _L.CONV_BIAS), ("lrelu", _L.CONV_LRELU),
+                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM),
+                 ("pixnorm", _L.CONV_PIXNORM)):
+        if f in fl:
+            flags |= v
+    Hin = H // 2 if "ups" in fl else H
+    x = q(rnd(B, Hin, Hin, cinp(cin), seed=91), dtype)
+    w = rnd(cout, cin, 3, 3, seed=92)
+    bias = rnd(cout, seed=93) * 0.1
+    Ho = H // 2 if "pool" in fl else H
+    y0 = q(rnd(B, Ho, Ho, cout, seed=94), dtype)
+    aux = q(rnd(B, H, H, cout, seed=95), dtype)
+    scale = 1.0 / (9 * cin) ** 0.5
+    outs = []
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        wp = torch.zeros(ops.packed_elems(0, cout, cin), dtype=dt, device=dev)
+        ops.conv_pack(0, w.to(dev), scale, wp)
+        y = y0.to(dev).to(dt).clone()
+        y2 = None
+        if "pool" in fl:
+            y2 = torch.zeros(B, H, H, cout, dtype=dt, device=dev)
+        if "pixnorm" in fl:
+            y2 = torch.zeros(B, H, H, dtype=torch.float32, device=dev)
+        ops.conv3x3(x.to(dev).to(dt), wp, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
+                    slope=0.2, out_scale=0.25 if "pool" in fl else 1.0,
+                    bias=(bias * scale).to(dev), aux=aux.to(dev).to(dt), y2=y2)
+        outs.append((y, y2))
+    cmp(outs[0][0], outs[1][0], 2e-2, "kg y")
+    if outs[0][1] is not None:
+        cmp(outs[0][1], outs[1][1], 2e-2, "kg y2")
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_conv_pack_batch(dtype):
     """One batched launch == the per-layer fwd / dgrad packs and scaled biases, bit-exact."""
