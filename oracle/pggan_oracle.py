@@ -343,7 +343,7 @@ class StepOut:
 
 def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
                W_adv=1.0, slope_cfg=0.2, gp_mode="r1", gp_eps=None, W_gp=10.0, W_drift=0.0,
-               kinks=None, fake_D=None, fake_G=None):
+               kinks=None, fake_D=None, fake_G=None, grads_D_update=None):
     """pggan/model.py:206-255 ProgressiveGAN.train_step on CPU; updates PG/PD in place.
 
     gp_mode="r1" is the live reference path (pggan/loss.py:16-27).
@@ -358,6 +358,9 @@ def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
     place of this G's output (parity tests, to compare each network on identical inputs;
     the G half keeps this G's gradient path: the value is fake_G, the gradient flows
     into this G).  The returned img_fake_* are always this G's own outputs.
+    grads_D_update: optional D gradient that Adam_D applies instead of this step's own (the
+    data-parallel contract: every rank's G half runs with D updated by the mean over ranks;
+    tests/test_gpu_dp.py); the returned grads_D are still this step's own.
     Works in any floating dtype (the tests run it in float64)."""
     kD = list(kinks["D"]) if kinks else []
     kG = list(kinks["G"]) if kinks else []
@@ -394,7 +397,7 @@ def train_step(PG, PD, optG, optD, img_real, z1, z2, s, alpha_G, alpha_D,
     gd = torch.autograd.grad(L_D, [PD[k] for k in dkeys], allow_unused=True)
     grads_D = dict(zip(dkeys, gd))
     with torch.no_grad():
-        optD.update(PD, grads_D)                                    # lib/utils.py:72-75
+        optD.update(PD, grads_D if grads_D_update is None else grads_D_update)   # lib/utils.py:72-75
 
     img_fake_G = G(PG, z2)                                          # :244-245
     img_fake_G_own = img_fake_G

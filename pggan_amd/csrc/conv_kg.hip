@@ -53,7 +53,8 @@ struct KgParams {
   float slope, out_scale;
   int lg_tx, lg_ty;
   int xcd_remap;
-  int diag;   // timing diagnostics (PG_KG_DIAG, wrong results): 1 no staging DMA, 4 no epilogue
+  int diag;   // timing diagnostics (PG_KG_DIAG, wrong results): 1 no staging DMA, 4 no epilogue,
+              // 8 / 16 contiguous weight / halo pieces (the feed with full-line requests)
 };
 
 // TH rows per tile; ONE: a single staging slot (LDS small enough for two workgroups per CU,
@@ -150,10 +151,14 @@ void conv_kg_kernel(KgParams p) {
       const int yy = ty0 + hy - 1, xx = tx0 + hx - 1;
       if (P < G::HPIX && (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W)
         v = (unsigned)((((yy >> ys) * p.Win + (xx >> ys)) * p.x_cs + 8 * j) * 2);
+      // feed diagnostic (PG_KG_DIAG & 16, wrong results): the same bytes as contiguous 1-KiB runs
+      if (p.diag & 16) v = (unsigned)((((ty0 * p.Win + tx0) * p.x_cs) * 2 + sl * 16) & 0x3fffff);
     } else if (q < G::NP) {
       const int sl = (q - G::HPIECES) * 64 + lane, nr = sl / 36, sr = sl - nr * 36;
       const int tap = sr >> 2, j = (sr & 3) ^ kg_swz(nr);
       v = (unsigned)((((n0 + nr) * 9 + tap) * p.cin_p + 8 * j) * 2);
+      // (PG_KG_DIAG & 8: the weight slab as one contiguous run, as a chunk-major packing gives)
+      if (p.diag & 8) v = (unsigned)(n0 * 9 * p.cin_p * 2 + sl * 16);
     }
     return v;
   };
@@ -475,7 +480,8 @@ int kg_variant(const pg_conv_desc* d) {
   const int cin_p = (d->cin + 31) & ~31;
   const bool pool = (d->flags & PG_CONV_POOL) != 0;
   if (mode == 2) return d->H >= 256 && cin_p <= 64 ? -16 : d->H >= 128 ? 32 : d->H >= 64 ? 16 : 8;
-  if (d->H >= 256 && cin_p <= 64) return -16;
+  // (with MASK the one-slot form is slower: its mask operands spill at 128 registers)
+  if (d->H >= 256 && cin_p <= 64 && !(d->flags & PG_CONV_MASK)) return -16;
   if (d->H == 64 && !pool) return 16;
   return 0;
 }

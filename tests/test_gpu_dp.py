@@ -4,10 +4,12 @@ gloo process group, HipOps kernels, the product path's bucketed asynchronous exc
 
 Contract (tests/test_dp_gloo.py states it on the CPU double): the DP D gradient equals the
 mean over ranks of the single-process reference D gradient on each rank's shard (NOT one
-global-batch step: R1 scales as 1/B^2), and parameters and G gradients are bit-identical
-across ranks after both Adam steps.  The per-shard reference is the float64 oracle replayed
-with that rank's leaky-ReLU region choices (tests/kink_parity.py), so every D tensor is
-held to 1e-3.
+global-batch step: R1 scales as 1/B^2); the DP G gradient equals the mean over ranks of the
+reference G gradient of each shard's G half run against D updated with that mean D gradient
+(what every rank's G half sees); the parameters after both Adam steps equal the reference
+Adam updates with those mean gradients; and parameters and gradients are bit-identical
+across ranks.  The per-shard reference is the float64 oracle replayed with that rank's
+leaky-ReLU region choices (tests/kink_parity.py), so every gradient tensor is held to 1e-3.
 """
 import os
 import socket
@@ -79,6 +81,9 @@ def _worker(rank, world, port, out_dir, reduce_bf16=False):
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), gD=fpD.grad.cpu().numpy(),
              gG=fpG.grad.cpu().numpy(), pD=fpD.flat.cpu().numpy(), pG=fpG.flat.cpu().numpy(),
              gD_ref=gD_ref, n_live=fpD.n_live)
+    # the region choices of this rank's forwards, for the G-half replay with the mean D update
+    torch.save({n: [k.masks for k in rec.seq[n]] for n in ("D", "G")},
+               os.path.join(out_dir, f"rank{rank}_kinks.pt"))
     dist.destroy_process_group()
 
 
@@ -112,3 +117,62 @@ def test_dp_two_ranks_on_hip_kernels(tmp_path, reduce):
         else:
             err = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
         assert err <= (1e-2 if reduce == "bf16" else 1e-3), (n, err)
+    _check_g_and_params(tmp_path, r, world, reduce)
+
+
+def _check_g_and_params(tmp_path, r, world, reduce):
+    """The G gradient and both nets' parameters against the float64 oracle: each rank's step
+    replayed with its kinks and Adam_D fed the mean D gradient (the DP run's), then the mean of
+    the per-rank G gradients and the Adam updates of the initial parameters with the means."""
+    import kink_parity as K
+    from oracle import pggan_oracle as O
+    from pggan_amd import engine as E
+    gsh, dsh = E.g_param_shapes(TINY_DEPTHS, S), E.d_param_shapes(TINY_DEPTHS, S)
+    fpD = E.FlatParams(dsh, E.dead_params("D", S), "cpu")
+    fpG = E.FlatParams(gsh, E.dead_params("G", S), "cpu")
+    PG0 = {k: torch.from_numpy(v).double() for k, v in make_params(gsh, seed=801).items()}
+    PD0 = {k: torch.from_numpy(v).double() for k, v in make_params(dsh, seed=802).items()}
+    gD_mean = sum(x["gD_ref"] for x in r) / world
+    gD_upd = {n: (None if n in fpD.dead else
+                  torch.from_numpy(gD_mean[fpD.offsets[n]:fpD.offsets[n] + int(np.prod(fpD.shapes[n]))])
+                  .view(fpD.shapes[n])) for n in fpD.names}
+    gG_list, pD_ref = [], None
+    for rank in range(world):
+        km = torch.load(tmp_path / f"rank{rank}_kinks.pt", weights_only=True)
+        kinks = {n: [O.Kinks(m) for m in km[n]] for n in ("D", "G")}
+        st = make_inputs(B, 4 * 2 ** S, seed=900 + rank)[0]
+        real, z1, z2 = (torch.from_numpy(st[k]).double() for k in ("real", "z1", "z2"))
+        PG = {k: v.clone() for k, v in PG0.items()}
+        PD = {k: v.clone() for k, v in PD0.items()}
+        optG, optD = O.AdamState(1e-4), O.AdamState(1e-5)
+        ref = O.train_step(PG, PD, optG, optD, real, z1, z2, S, ALPHA, ALPHA, kinks=kinks,
+                           grads_D_update=gD_upd)
+        gG_list.append({k: (None if v is None else v.clone()) for k, v in ref.grads_G.items()})
+        pD_ref = PD   # the same on every rank: Adam_D applied the mean gradient
+    gG_mean = {k: (None if gG_list[0][k] is None else sum(g[k] for g in gG_list) / world)
+               for k in gG_list[0]}
+    PG = {k: v.clone() for k, v in PG0.items()}
+    O.AdamState(1e-4).update(PG, gG_mean)
+    pG_ref = PG
+    gG_ours = torch.from_numpy(r[0]["gG"]).double()
+    pG_ours = torch.from_numpy(r[0]["pG"]).double()
+    pD_ours = torch.from_numpy(r[0]["pD"]).double()
+    tol = 1e-2 if reduce == "bf16" else 1e-3
+    for n in fpG.names:
+        if n in fpG.dead:
+            continue
+        o, c = fpG.offsets[n], int(np.prod(fpG.shapes[n]))
+        a, b = gG_ours[o:o + c], gG_mean[n].ravel()
+        if reduce == "bf16":   # relative to the addends' magnitude (see the D check above)
+            scale = sum(g[n].abs().ravel() for g in gG_list) / world
+            err = float((a - b).norm()) / max(float(scale.norm()), 1e-30)
+        else:
+            err = K.rel_l2(a, b)
+        assert err <= tol, ("G grad", n, err)
+    # beta1 = 0: the first Adam update is ~lr * sign(g), so a last-bit difference of a near-zero
+    # gradient moves a parameter by up to 2 lr (lr_G = 1e-4, lr_D = 1e-5)
+    for (ours, refp, fp, lr, what) in ((pG_ours, pG_ref, fpG, 1e-4, "G"), (pD_ours, pD_ref, fpD, 1e-5, "D")):
+        for n in fp.names:
+            o, c = fp.offsets[n], int(np.prod(fp.shapes[n]))
+            d = float((ours[o:o + c] - refp[n].ravel()).abs().max())
+            assert d <= 2 * lr + 1e-6, (what, "param", n, d)

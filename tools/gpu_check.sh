@@ -1,6 +1,9 @@
 #!/bin/bash
-# GPU-box check: each GPU step under its own time limit; stops at the first step that
-# ends other than pass (0) / test failures (1).  Logs under gpurun_out/.
+# GPU-box runner: `bash tools/gpu_check.sh STEP [STEP ...]`, each GPU step under its own time
+# limit; stops at the first step that ends other than pass (0) / test failures (1).  Logs under
+# gpurun_out/<step>.log.  The steps are the measurement recipes DESIGN.md cites (suite, smoke,
+# bench, kernel trace + PMC passes, kbench shape lists, probes, loader, configs, DP rehearsal);
+# interleaved A/B runs of library knobs or builds: tools/ab.sh.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -79,9 +82,20 @@ for step in "$@"; do
           -d "$ROOT/gpurun_out/kprof" -o run -- python "$ROOT/tools/kbench.py" --iters 5 ${KPROF_SPECS} ) \
           > gpurun_out/kprof.log 2>&1
       rc=$?; echo "kprof rc=$rc"; tail -n 3 gpurun_out/kprof.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
-    pdsweep) run pdsweep 900 bash tools/pd_sweep.sh ;;
     opprof) run opprof 300 python tools/op_profile.py --json gpurun_out/opprof.json ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
+    kloop) run kloop 120 ./tools/kloop_probe ;;   # build: hipcc --offload-arch=gfx950 -O3 -o tools/kloop_probe tools/kloop_probe.hip
+    kgdiag)   # conv_kg with its staging / epilogue switched off or fed contiguously (PG_KG_DIAG)
+      for dg in 0 8 16 24 1 4; do
+        PG_KG=2 PG_KG_DIAG=$dg run kgdiag_$dg 120 python tools/kbench.py --iters 30 c:32:512:512:0 \
+          c:64:256:256:0 c:128:128:128:0 c:256:64:64:0 c:256:128:64:8
+      done ;;
+    kg) run kg 300 python -m pytest tests/test_gpu_ops.py -q -x -k "conv_kg or conv3x3_fwd or sign_bit" ;;
+    dp) run dp 600 python -u -m pytest tests/test_gpu_dp.py -x -q --timeout 300 --timeout-method thread ;;
+    graph) run graph 600 python -u -m pytest tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread ;;
+    loader) run loader 600 python tools/loader_bench.py --out gpurun_out/loader.json ;;
+    configs) run configs 1500 bash tools/configs_bench.sh ;;
+    rehearsal) run rehearsal 900 bash tools/dp_rehearsal.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

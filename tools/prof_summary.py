@@ -67,10 +67,50 @@ def group_traffic(path_fetch, path_write, launches_json):
         g["calls"] += 1
         g["hbm_bytes"] += (2.0 * fv + wv) * 1024.0
         g["alg_bytes"] += L["bytes"]
-    return {k: dict(calls=v["calls"], hbm_bytes_per_call=v["hbm_bytes"] / v["calls"],
-                    alg_bytes_per_call=v["alg_bytes"] / v["calls"],
-                    traffic_over_alg=v["hbm_bytes"] / max(v["alg_bytes"], 1.0))
-            for k, v in groups.items()}
+    out = {k: dict(calls=v["calls"], hbm_bytes_per_call=v["hbm_bytes"] / v["calls"],
+                   alg_bytes_per_call=v["alg_bytes"] / v["calls"],
+                   traffic_over_alg=v["hbm_bytes"] / max(v["alg_bytes"], 1.0))
+           for k, v in groups.items()}
+    per_call = [(L, (2.0 * fv + wv) * 1024.0) for L, (_, fv), (_, wv) in zip(launches, fe, wr)]
+    return out, per_call
+
+
+def trace_calls(path, n):
+    """Durations (ns) of the last n conv / wgrad calls of a kernel trace in dispatch (= host
+    issue) order, a call = its main kernel + the split epilogue / slab reduction after it."""
+    path = _resolve(path, "kernel_trace.csv")
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            fm, is_call = family(r["Kernel_Name"])
+            if fm:
+                rows.append((int(r["Dispatch_Id"]), is_call,
+                             int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    rows.sort()
+    out = []
+    for _, is_call, d in rows:
+        if is_call or not out:
+            out.append(0)
+        out[-1] += d
+    return out[-n:]
+
+
+def per_resolution(per_call, durations):
+    """North star's HBM view per resolution (conv + weight-gradient launches): PMC-measured
+    HBM bytes (FETCH x2 + WRITE) over the kernel-trace durations of the same calls, next to
+    the algorithmic bytes."""
+    rows = defaultdict(lambda: dict(calls=0, hbm_bytes=0.0, alg_bytes=0.0, ns=0))
+    for (L, hb), ns in zip(per_call, durations):
+        r = rows[L["H"]]
+        r["calls"] += 1
+        r["hbm_bytes"] += hb
+        r["alg_bytes"] += L["bytes"]
+        r["ns"] += ns
+    return [dict(res=H, calls=r["calls"], ms=round(r["ns"] / 1e6, 4),
+                 hbm_mb=round(r["hbm_bytes"] / 1e6, 2), alg_mb=round(r["alg_bytes"] / 1e6, 2),
+                 hbm_gbps=round(r["hbm_bytes"] / max(r["ns"], 1), 1),
+                 hbm_frac=round(r["hbm_bytes"] / max(r["ns"], 1) / 8000.0, 4))
+            for H, r in sorted(rows.items())]
 
 
 def short(name):
@@ -177,7 +217,15 @@ def main():
                                              dispatches=f[1])
                                      for n, f in sorted(fper.items(), key=lambda kv: -kv[1][0])[:25]}
         if a.launches:
-            res["groups"] = group_traffic(a.fetch, a.write, a.launches)
+            res["groups"], per_call = group_traffic(a.fetch, a.write, a.launches)
+            try:
+                res["per_resolution"] = per_resolution(per_call, trace_calls(a.trace, len(per_call)))
+                res["per_resolution_note"] = (
+                    "conv + weight-gradient calls of one step: hbm_mb = PMC FETCH_SIZE x2 + "
+                    "WRITE_SIZE (separate --pmc passes), ms = the same calls' kernel-trace "
+                    "durations (two streams: calls overlap, so a row's GB/s is per call time)")
+            except (AssertionError, KeyError, ValueError) as e:
+                res["per_resolution_error"] = str(e)
         res["pmc_note"] = ("bytes/call = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 summed over the "
                            "family's dispatches of the PMC passes / the family's calls; "
                            "calibrate with adam_kernel: 28 B per parameter (4 fp32 reads, 3 writes)")
