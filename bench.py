@@ -98,11 +98,18 @@ class KernelTimer:
         self.shapes = []
         self.on = False
         f_conv, f_wg = ops.conv3x3, ops.conv_wgrad
+        # timing events without the system-scope fence (pg_event_create(timing=1)): a torch
+        # timing event writes back and invalidates every XCD's L2 at each record, so the
+        # launch it brackets would start cold and ~6.5 us late
+        if os.environ.get("PG_TORCH_EVENTS", "0") == "1":
+            self.ev = lambda: torch.cuda.Event(enable_timing=True)
+        else:
+            self.ev = lambda: ops.event(timing=True)
 
         def conv3x3(x, wpk, y, **kw):
             if not self.on:
                 return f_conv(x, wpk, y, **kw)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a, b = self.ev(), self.ev()
             a.record()
             f_conv(x, wpk, y, **kw)
             b.record()
@@ -115,7 +122,7 @@ class KernelTimer:
         def conv_wgrad(x, gz, dw, **kw):
             if not self.on:
                 return f_wg(x, gz, dw, **kw)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a, b = self.ev(), self.ev()
             a.record()
             f_wg(x, gz, dw, **kw)
             b.record()

@@ -326,6 +326,18 @@ size_t pg_augment_workspace_bytes(int B, int H, int W);
 int pg_augment_u8(int B, int H, int W, const void* src, const float* params, float* ws,
                   size_t ws_bytes, float* dst, void* stream);
 
+/* ---- stream ordering between the engine's streams (weight gradients on a side stream).
+ * torch's cross-stream events record with a system-scope release: every record writes back and
+ * invalidates the L2 of all XCDs and the next kernel on that stream starts ~6.5 us late.  The
+ * two streams are on one device, so these events release to device scope only
+ * (hipEventReleaseToDevice).  `timing` != 0: a timing event that also skips the system fence
+ * (hipEventDisableSystemFence), for the bench's per-launch timers.  Handles are opaque. */
+int pg_event_create(int timing, void** ev);
+int pg_event_record(void* ev, void* stream);
+int pg_stream_wait_event(void* stream, void* ev);
+int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);
+int pg_event_destroy(void* ev);
+
 /* ---- step plan: the kernel path of every 3x3 conv pass (forward, input
  * gradient, weight gradient) of one train_step at (stage, batch, dtype) -- the layer list of
  * pggan/nets.py:53-119 (G) and :164-239 (D) at scale_index = stage -- and the split-reduction

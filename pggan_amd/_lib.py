@@ -151,6 +151,11 @@ _SIGS = {
     "pg_step_plan_workspace_size": ([_VP], _SZ),
     "pg_step_plan_describe": ([_VP, ctypes.c_char_p, _SZ], _I),
     "pg_step_plan_destroy": ([_VP], None),
+    "pg_event_create": ([_I, ctypes.POINTER(ctypes.c_void_p)], _I),
+    "pg_event_record": ([_VP, _VP], _I),
+    "pg_stream_wait_event": ([_VP, _VP], _I),
+    "pg_event_elapsed_ms": ([_VP, _VP, ctypes.POINTER(ctypes.c_float)], _I),
+    "pg_event_destroy": ([_VP], _I),
 }
 SYMBOLS = ["pg_last_error"] + list(_SIGS)
 
@@ -179,6 +184,46 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+class HipEvent:
+    """A HIP event from pg_event_create: record on / wait from torch streams.  Unlike
+    torch.cuda.Event its record releases to device scope only (no L2 writeback / invalidate
+    of every XCD per record), which is all that ordering two streams of one device needs."""
+
+    def __init__(self, ops, timing=False):
+        self.lib = ops.lib
+        h = ctypes.c_void_p()
+        ops._chk(self.lib.pg_event_create(int(bool(timing)), ctypes.byref(h)), "event_create")
+        self.h = h
+
+    def record(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = self.lib.pg_event_record(self.h, ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"event_record failed ({rc}): {self.lib.pg_last_error().decode()}")
+
+    def wait(self, stream=None):
+        """Make `stream` (default: current) wait for this event's last record."""
+        s = stream if stream is not None else torch.cuda.current_stream()
+        rc = self.lib.pg_stream_wait_event(ctypes.c_void_p(s.cuda_stream), self.h)
+        if rc != 0:
+            raise RuntimeError(f"stream_wait_event failed ({rc}): {self.lib.pg_last_error().decode()}")
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        rc = self.lib.pg_event_elapsed_ms(self.h, end.h, ctypes.byref(ms))
+        if rc != 0:
+            raise RuntimeError(f"event_elapsed_ms failed ({rc}): {self.lib.pg_last_error().decode()}")
+        return ms.value
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h is not None and h.value:
+            try:
+                self.lib.pg_event_destroy(h)
+            except Exception:
+                pass
+
+
 class HipOps:
     """Tensor-level wrappers of the C ABI.  `dtype` = storage dtype of activations."""
 
@@ -204,6 +249,11 @@ class HipOps:
 
     def _dt(self, t):
         return PG_F32 if t.dtype == torch.float32 else PG_BF16
+
+    # -- stream ordering -----------------------------------------------------
+    def event(self, timing=False):
+        """A HipEvent (device-scope release; see pg_event_create)."""
+        return HipEvent(self, timing)
 
     # -- step plan ---------------------------------------------------------
     def step_plan(self, depths, stage, batch):

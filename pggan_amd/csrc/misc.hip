@@ -1815,6 +1815,45 @@ int pg_adam_dev(size_t n, float* p, const float* g, float* m, float* v, float be
   return PG_OK;
 }
 
+// ---- cross-stream events with a device-scope release (include/pggan_hip.h)
+static int pg_hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return PG_OK;
+  pg_set_error("%s: %s", what, hipGetErrorString(e));
+  return PG_ERR_HIP;
+}
+
+int pg_event_create(int timing, void** ev) {
+  PG_CHECK_ARG(ev, "event_create: null out");
+  const unsigned flags = timing ? (hipEventDisableSystemFence | hipEventReleaseToDevice)
+                                : (hipEventDisableTiming | hipEventReleaseToDevice);
+  hipEvent_t e = nullptr;
+  const int rc = pg_hip_status(hipEventCreateWithFlags(&e, flags), "hipEventCreateWithFlags");
+  *ev = rc == PG_OK ? (void*)e : nullptr;
+  return rc;
+}
+
+int pg_event_record(void* ev, void* stream) {
+  PG_CHECK_ARG(ev, "event_record: null event");
+  return pg_hip_status(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+}
+
+int pg_stream_wait_event(void* stream, void* ev) {
+  PG_CHECK_ARG(ev, "stream_wait_event: null event");
+  return pg_hip_status(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0),
+                       "hipStreamWaitEvent");
+}
+
+int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms) {
+  PG_CHECK_ARG(ev_start && ev_end && ms, "event_elapsed_ms: null argument");
+  return pg_hip_status(hipEventElapsedTime(ms, (hipEvent_t)ev_start, (hipEvent_t)ev_end),
+                       "hipEventElapsedTime");
+}
+
+int pg_event_destroy(void* ev) {
+  if (!ev) return PG_OK;
+  return pg_hip_status(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy");
+}
+
 int pg_randn_dev(size_t n, uint64_t seed, uint64_t* offset, float* out, void* stream) {
   PG_CHECK_ARG(out && offset, "randn_dev: null pointer");
   hipStream_t st = (hipStream_t)stream;

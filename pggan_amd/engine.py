@@ -241,7 +241,25 @@ class StepEngine:
         if self.side is not None and os.environ.get("PG_FAKE_STREAM", "0") == "1":
             self.fstream = torch.cuda.Stream(device=device)
             self.side2 = torch.cuda.Stream(device=device)
+        # the cross-stream events: the library's device-scope-release events (pg_event_create)
+        # from a ring.  torch's events release to system scope -- each record writes back and
+        # invalidates every XCD's L2 and delays the stream's next kernel by ~6.5 us, and the step
+        # records ~75 of them.  A ring slot is re-recorded only after 512 more records; a wait
+        # always binds the record made before it, and a join that meets a re-recorded slot waits
+        # for a later point of the side stream (more ordering, never less).
+        # PG_TORCH_EVENTS=1: torch.cuda.Event (A/B runs).
+        self._ev_ring, self._ev_i = None, 0
+        if (self.side is not None and hasattr(ops, "event") and
+                os.environ.get("PG_TORCH_EVENTS", "0") != "1"):
+            self._ev_ring = [ops.event() for _ in range(512)]
         self._alloc()
+
+    def _event(self):
+        if self._ev_ring is None:
+            return None
+        ev = self._ev_ring[self._ev_i]
+        self._ev_i = (self._ev_i + 1) % len(self._ev_ring)
+        return ev
 
     # ------------------------------------------------------------------ buffers
     def _t(self, *shape, f32=False):
@@ -472,13 +490,22 @@ class StepEngine:
         written on the main stream, so the side stream first waits for it."""
         if self.side is None or FORCE_SERIAL:
             return fn(*a, **kw)
-        self.side.wait_stream(torch.cuda.current_stream())
+        self._side_wait_main()
         with torch.cuda.stream(self.side):
             fn(*a, **kw)
-        ev = torch.cuda.Event()
+        ev = self._event() or torch.cuda.Event()
         ev.record(self.side)
         for n in nets:
             self._side_ev[self._dkey if n == "D" else n] = ev
+
+    def _side_wait_main(self):
+        """The side stream waits for everything enqueued on the current stream so far."""
+        ev = self._event()
+        if ev is None:
+            self.side.wait_stream(torch.cuda.current_stream())
+        else:
+            ev.record(torch.cuda.current_stream())
+            ev.wait(self.side)
 
     def _side_join(self, net=None):
         """Order the side-stream launches that read `net`'s buffers (all of them when None;
@@ -494,7 +521,10 @@ class StepEngine:
         for k in keys:
             ev = self._side_ev.pop(k, None)
             if ev is not None:
-                cur.wait_event(ev)
+                if isinstance(ev, torch.cuda.Event):
+                    cur.wait_event(ev)
+                else:
+                    ev.wait(cur)
 
     def _dbits(self, i):
         """Whether D level i keeps its conv-b (conv + lrelu + pool) output as sign bits only:
@@ -720,7 +750,7 @@ class StepEngine:
         # the gradients come from both streams: the side stream waits for the main one and
         # the callback runs on it, so a collective it starts sees both without stalling the
         # main stream's next convs
-        self.side.wait_stream(torch.cuda.current_stream())
+        self._side_wait_main()
         with torch.cuda.stream(self.side):
             self.grad_ready(net, names)
 
