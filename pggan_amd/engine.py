@@ -223,6 +223,8 @@ class StepEngine:
         # gradient (see _side_join).  PG_SIDE_WGRAD=0 keeps one stream (A/B runs).
         self.side = None
         self._side_ev = {}      # buffer-set key -> last side-stream event reading it
+        self._side_pending = []  # queued side launches (side_batch > 1, see _side_call)
+        self.side_batch = max(1, int(os.environ.get("PG_SIDE_BATCH", "1")))
         self.ws_side = None
         self._dkey = "D"        # key of the D buffer set in use ("Df": the fake-image pass)
         if (forward_only is None and str(device).startswith("cuda") and
@@ -241,6 +243,13 @@ class StepEngine:
         if self.side is not None and os.environ.get("PG_FAKE_STREAM", "0") == "1":
             self.fstream = torch.cuda.Stream(device=device)
             self.side2 = torch.cuda.Stream(device=device)
+        # PG_MAIN_PRIORITY=1 (A/B runs): the step's main stream (the input-gradient chain, the
+        # critical path) is a high-priority stream, so the dispatcher serves its workgroups
+        # before the side stream's weight gradients when both have work queued
+        self.main_hp = None
+        if self.side is not None and os.environ.get("PG_MAIN_PRIORITY", "0") == "1":
+            self.main_hp = torch.cuda.Stream(device=device,
+                                             priority=torch.cuda.Stream.priority_range()[1])
         # the cross-stream events: the library's device-scope-release events (pg_event_create)
         # from a ring.  torch's events release to system scope -- each record writes back and
         # invalidates every XCD's L2 and delays the stream's next kernel by ~6.5 us, and the step
@@ -478,6 +487,7 @@ class StepEngine:
         need = self._ws_bytes("w", H, cin, cout, ups)
         if need and (self.ws_side is None or self.ws_side.numel() * 4 < need):
             # the side stream may still read the old workspace
+            self._side_flush()
             self.side.synchronize()
             self.ws_side = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         self._side_call((net,), self.ops.conv_wgrad, x, gz, dW, B=self.B, H=H, W=H, cin=cin,
@@ -487,16 +497,30 @@ class StepEngine:
     def _side_call(self, nets, fn, *a, **kw):
         """Run a weight-gradient launch `fn` on the side stream (or inline without one).
         nets: whose buffers it reads (joins before those are overwritten).  Its inputs were
-        written on the main stream, so the side stream first waits for it."""
+        written on the main stream, so the side stream first waits for it.  With
+        side_batch > 1 the launches are queued on the host and enqueued side_batch at a time
+        behind ONE main-stream event (each event record costs the main stream's next kernel
+        ~6.5 us); _side_flush() also runs at every join, before a grad_ready callback and
+        before the side workspace is replaced."""
         if self.side is None or FORCE_SERIAL:
             return fn(*a, **kw)
+        self._side_pending.append((nets, fn, a, kw))
+        if len(self._side_pending) >= self.side_batch:
+            self._side_flush()
+
+    def _side_flush(self):
+        if not self._side_pending:
+            return
+        pend, self._side_pending = self._side_pending, []
         self._side_wait_main()
         with torch.cuda.stream(self.side):
-            fn(*a, **kw)
+            for _, fn, a, kw in pend:
+                fn(*a, **kw)
         ev = self._event() or torch.cuda.Event()
         ev.record(self.side)
-        for n in nets:
-            self._side_ev[self._dkey if n == "D" else n] = ev
+        for nets, *_ in pend:
+            for n in nets:
+                self._side_ev[self._dkey if n == "D" else n] = ev
 
     def _side_wait_main(self):
         """The side stream waits for everything enqueued on the current stream so far."""
@@ -514,6 +538,7 @@ class StepEngine:
         reads the gradients and at the end of each half-step (so callers reading gradients
         need no stream handling).  Events, not stream waits: a join never waits for side
         work of the other buffer set."""
+        self._side_flush()
         if not self._side_ev:
             return
         keys = list(self._side_ev) if net is None else [self._dkey if net == "D" else net]
@@ -750,6 +775,7 @@ class StepEngine:
         # the gradients come from both streams: the side stream waits for the main one and
         # the callback runs on it, so a collective it starts sees both without stalling the
         # main stream's next convs
+        self._side_flush()
         self._side_wait_main()
         with torch.cuda.stream(self.side):
             self.grad_ready(net, names)
@@ -1012,6 +1038,7 @@ class StepEngine:
             buf = torch.zeros_like(self.fpD.grad)
             gd2 = self._gd2 = (self.fpD, buf, {n: self.fpD._view(buf, n) for n in self.fpD.names})
         _, buf, views = gd2
+        self._side_flush()     # queued launches belong to the main pass's side stream
         saved = (self.dd, self.ws, self.side, self.ws_side, self._dkey)
         fs.wait_event(ev0)
         with torch.cuda.stream(fs):
@@ -1111,6 +1138,19 @@ class StepEngine:
                       beta2=hp.beta2, eps=hp.eps, step=fp.step)
 
     def train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
+        """_train_step on the high-priority main stream when PG_MAIN_PRIORITY=1 (see
+        __init__), ordered after and back into the caller's stream."""
+        hs = self.main_hp
+        if hs is None or torch.cuda.is_current_stream_capturing():
+            return self._train_step(real, z1, z2, alpha_G, alpha_D, grad_hook, gp_eps)
+        cur = torch.cuda.current_stream()
+        hs.wait_stream(cur)
+        with torch.cuda.stream(hs):
+            out = self._train_step(real, z1, z2, alpha_G, alpha_D, grad_hook, gp_eps)
+        cur.wait_stream(hs)
+        return out
+
+    def _train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
         """One full step: D half (R1) + Adam_D, G half + Adam_G (pggan/model.py:206-255).
 
         grad_hook(net, flat_live_grad) runs before each Adam (DP all-reduce).  If it returns

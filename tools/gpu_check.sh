@@ -10,8 +10,12 @@ mkdir -p gpurun_out
 run() {
   local name=$1; shift
   local t=$1; shift
+  # heartbeat: the CPU oracle of the largest parity cases runs for minutes without output
+  ( while sleep 50; do date +%T >> gpurun_out/heartbeat.log; done ) &
+  local hb=$!
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "$name rc=$rc"
   tail -n 3 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
@@ -20,7 +24,7 @@ for step in "$@"; do
   case $step in
     ops) run ops 900 python -m pytest tests/test_gpu_ops.py -q -x ;;
     parity) run parity 1200 python -m pytest tests/test_gpu_parity.py -q ;;
-    gpu) run gpu 1500 python -m pytest tests -q -m gpu ;;
+    gpu) run gpu 1500 python -u -m pytest tests -v -m gpu --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps 20 --warmup 5 ;;
     benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --cpu-baseline off ;;
