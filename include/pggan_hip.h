@@ -61,9 +61,12 @@ int pg_version(void);
  * holds the leaky-relu sign (activation > 0) of every channel: [B][H][W][bytes], channel c
  * at byte c/8, bit c%8.  1 bit replaces a 16-bit activation wherever only its sign is read
  * again (the discriminator's conv+LReLU+pool outputs, lib/blocks.py:189-193). */
-#define PG_CONV_Y2_BITS 128   /* with POOL: y2 receives the sign bits of the pre-pool output */
+#define PG_CONV_Y2_BITS 128   /* y2 receives the sign bits of the activated output: with POOL
+                                 of the pre-pool output; without POOL (16 / 32 output channels)
+                                 of y itself, the lrelu' operand of the layer's later masks */
 #define PG_CONV_AUX_BITS 256  /* MASK operand aux is a bit tensor (aux_cs = bytes per pixel);
-                                 with POOL the mask applies before pooling */
+                                 with POOL the mask applies before pooling; may be combined
+                                 with X_BITS (input and output masks both from bits) */
 #define PG_CONV_X_BITS 512    /* x is masked on load by lrelu'(xbits) at conv resolution
                                  (pg_conv3x3_fwd_ex; xb_cs = bytes per pixel) */
 #define PG_CONV_GZ_BITS 1024  /* wgrad: gz is at H/2 x W/2 and the effective gradient is
@@ -202,6 +205,14 @@ typedef struct {
 int pg_from_rgb_src(int dtype, int B, int R, int C, const pg_img_src* img, int down, const float* w,
                     const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
                     void* stream);
+/* pg_from_rgb_src (bf16, C % 8 == 0, C <= 64) with the lrelu sign bits as an operand instead of
+ * a bf16 activation: ybits != NULL (forward) also writes the bits of the result y > 0, uint8
+ * [B][R][R][C / 8] (channel o at byte o / 8, bit o % 8); mask_bits != NULL (the R1 tangent) masks
+ * with those bits where pg_from_rgb reads mask_y (16x fewer bytes: 134 MB -> 8.4 MB per launch at
+ * 1024^2, 16 channels, B = 4).  At most one of the two. */
+int pg_from_rgb_bits(int dtype, int B, int R, int C, const pg_img_src* img, int down,
+                     const float* w, const float* b, float c, float slope, const void* mask_bits,
+                     int y_cs, void* y, void* ybits, void* stream);
 /* pg_from_rgb_bwd with the image operand (of the weight gradient) as a pg_img_src, and for the
  * input gradient: gimg_overwrite = 1 writes gimg instead of accumulating into it; norms !=
  * NULL: norms[b] += sum over sample b of the final gimg^2 (the penalties' per-sample squared

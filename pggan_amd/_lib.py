@@ -117,6 +117,8 @@ _SIGS = {
     "pg_img_fade": ([_I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_from_rgb_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP, _I,
                          _VP, _VP], _I),
+    "pg_from_rgb_bits": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP,
+                          _I, _VP, _VP, _VP], _I),
     "pg_from_rgb_bwd_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _F, _I, _VP, _VP,
                              _I, _VP, _VP, _VP, _VP], _I),
     "pg_penalty_scale": ([_I, _I, _VP, _F, _VP, _VP, _VP], _I),
@@ -423,9 +425,18 @@ class HipOps:
         self._cuda(img)
         return ImgSrcDesc(img.data_ptr(), None, None, None)
 
-    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
-        self._cuda(w, b, y, mask_y)
+    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None, ybits=None,
+                 mask_bits=None):
+        """ybits: also write the lrelu sign bits of y (uint8 [B, R, R, C / 8]); mask_bits: the
+        tangent's lrelu' mask from those bits instead of mask_y (pg_from_rgb_bits)."""
+        self._cuda(w, b, y, mask_y, ybits, mask_bits)
         src = self._src(img)
+        if ybits is not None or mask_bits is not None:
+            self._chk(self.lib.pg_from_rgb_bits(self._dt(y), B, R, C, ctypes.byref(src),
+                                                1 if down else 0, _p(w), _p(b), c, slope,
+                                                _p(mask_bits), y.shape[-1], _p(y), _p(ybits),
+                                                self._s()), "from_rgb_bits")
+            return
         self._chk(self.lib.pg_from_rgb_src(self._dt(y), B, R, C, ctypes.byref(src), 1 if down else 0,
                                            _p(w), _p(b), c, slope, _p(mask_y), y.shape[-1], _p(y),
                                            self._s()), "from_rgb")

@@ -1482,6 +1482,22 @@ int pg_from_rgb_src(int dtype, int B, int R, int C, const pg_img_src* img, int d
                        (hipStream_t)stream);
 }
 
+int pg_from_rgb_bits(int dtype, int B, int R, int C, const pg_img_src* img, int down,
+                     const float* w, const float* b, float c, float slope, const void* mask_bits,
+                     int y_cs, void* y, void* ybits, void* stream) {
+  PG_CHECK_ARG(dtype == PG_BF16 && img && w && y && C % 8 == 0 && C <= 64 && y_cs >= C &&
+                   (!img->x1 || (img->a && img->c)),
+               "from_rgb_bits: bad args (bf16, C %% 8 == 0, C <= 64)");
+  PG_CHECK_ARG(!(mask_bits && ybits), "from_rgb_bits: mask_bits (tangent) or ybits (forward)");
+  if (try_from_rgb<bf16_t>(B, R, C, ImgSrc(*img), down, w, b, c, slope, nullptr, y_cs, (bf16_t*)y,
+                           (hipStream_t)stream, (const uint8_t*)mask_bits, (uint8_t*)ybits) != 0) {
+    pg_set_error("from_rgb_bits: unsupported layout (y_cs %d)", y_cs);
+    return PG_ERR_ARG;
+  }
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
 static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, int down,
                              const float* w, float c, int gz_cs, const void* gz, float* gimg, int ow,
                              float* norms, float* dw, float* db, hipStream_t st) {

@@ -323,6 +323,8 @@ class StepEngine:
         D = {}
         if need_D:
             D["yrgb"] = t(B, R, R, d[s])
+            # lrelu sign bits of the fromRGB output (see _rgbbits)
+            D["rgbb"] = torch.zeros(B, R, R, (d[s] + 7) // 8, dtype=torch.uint8, device=self.dev)
             if s >= 1:
                 D["yd"] = t(B, R // 2, R // 2, d[s - 1])
                 D["hblend"] = t(B, R // 2, R // 2, d[s - 1])
@@ -333,6 +335,10 @@ class StepEngine:
                 D[f"mb{i}"] = torch.zeros(B, Ri, Ri, (d[i] + 7) // 8, dtype=torch.uint8,
                                           device=self.dev)
                 D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
+                # lrelu sign bits of the conv-a output (the lrelu' operand of its consumers'
+                # masks where the kernels support it, see _abits)
+                D[f"ab{i}"] = torch.zeros(B, Ri, Ri, (d[i + 1] + 7) // 8, dtype=torch.uint8,
+                                          device=self.dev)
                 D[f"bf{i}"] = t(B, Ri, Ri, d[i])
                 D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
             D["m"] = t(B, 4, 4, self.mcs)
@@ -575,6 +581,44 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
+    def _abits(self, i):
+        """Whether D level i's conv a also writes the sign bits of its activation (Y2_BITS
+        without the pool) and the two launches that mask with lrelu'(a) -- the conv-b input
+        gradient and the R1 tangent of conv a -- read those bits instead of the bf16
+        activation: 16x fewer mask bytes (the 1024^2 16-channel mask is 134 MB at B = 4).
+        Only at the sign-bit levels (_dbits).  PG_ABITS=0: off (A/B runs)."""
+        key = ("abits", i, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            d, Ri, B = self.depths, 8 * 2 ** i, self.B
+            ok = bool(self._dbits(i) and os.environ.get("PG_ABITS", "1") != "0" and
+                      d[i + 1] % 16 == 0)
+            if ok:
+                ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i + 1],
+                        flags=L.CONV_BIAS | L.CONV_LRELU | L.CONV_Y2_BITS)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i + 1],
+                            flags=L.CONV_MASK | L.CONV_AUX_BITS)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i], cout=d[i + 1],
+                            flags=L.CONV_UPS_IN | L.CONV_X_BITS | L.CONV_AUX_BITS | L.CONV_MASK))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
+    def _rgbbits(self):
+        """Whether the top fromRGB layer also writes the sign bits of its output and its two
+        lrelu' consumers -- the input gradient of the top conv a and the fromRGB tangent --
+        mask from those bits instead of the bf16 activation (at >= the sign-bit resolution).
+        PG_RGBBITS=0: off (A/B runs)."""
+        key = ("rgbbits", 0, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            d, s, R, B = self.depths, self.s, self.R, self.B
+            ok = bool(f is not None and self.fuse_dbits and s >= 1 and
+                      os.environ.get("PG_RGBBITS", "1") != "0" and d[s] % 8 == 0 and
+                      d[s] <= 64 and R >= self.dbits_min_res and
+                      f(B=B, H=R, W=R, cin=d[s], cout=d[s], flags=L.CONV_MASK | L.CONV_AUX_BITS))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _pn_fused(self, H, cin, cout, flags):
         """Whether this generator conv can run PixelNorm in its epilogue (all output
         channels in one tile of the kernel the library picks for the shape)."""
@@ -731,7 +775,8 @@ class StepEngine:
         self._side_join("D")
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(img, P[fr.format(s) + "weight"], P[fr.format(s) + "bias"], he(3), D["yrgb"],
-                     B=B, R=R, C=d[s], down=False, slope=SLOPE)            # nets.py:255
+                     B=B, R=R, C=d[s], down=False, slope=SLOPE,            # nets.py:255
+                     **(dict(ybits=D["rgbb"]) if self._rgbbits() else {}))
         low = self._low(alpha)
         self._last_dlow = low
         if low:
@@ -740,7 +785,11 @@ class StepEngine:
         h = D["yrgb"]
         for i in reversed(range(s)):                                           # :260-265
             Ri = 8 * 2 ** i
-            self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
+            if self._abits(i):
+                self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1],
+                           L.CONV_LRELU | L.CONV_Y2_BITS, y2=D[f"ab{i}"])
+            else:
+                self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
             if self._dbits(i):
                 self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
                            L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS, y2=D[f"mb{i}"],
@@ -833,8 +882,11 @@ class StepEngine:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
                                 db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc)
                     ready(b)
+                ab = self._abits(i)
                 self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
-                           L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
+                           L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS |
+                           (L.CONV_AUX_BITS if ab else 0),
+                           aux=D[f"ab{i}"] if ab else D[f"a{i}"],
                            dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
             else:
                 ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
@@ -851,7 +903,10 @@ class StepEngine:
                             d[i + 1],
                             db=GR[a + "bias"])
                 ready(a)
-            if i == s - 1:
+            if i == s - 1 and self._rgbbits():
+                self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
+                           L.CONV_MASK | L.CONV_AUX_BITS, aux=D["rgbb"], dgrad=True)
+            elif i == s - 1:
                 self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
                            L.CONV_MASK, aux=D["yrgb"], dgrad=True)
             else:
@@ -921,8 +976,9 @@ class StepEngine:
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
         self._side_join("D")
         fr = "fromRGB_blocks.{}.fromRGB.module."
+        mk = dict(mask_bits=D["rgbb"]) if self._rgbbits() else dict(mask_y=D["yrgb"])
         ops.from_rgb(gbar, P[fr.format(s) + "weight"], None, he(3), D["trgb"], B=B, R=R, C=d[s],
-                     down=False, slope=SLOPE, mask_y=D["yrgb"])
+                     down=False, slope=SLOPE, **mk)
         self._side_call(("D",), ops.from_rgb_bwd,
                         D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
                         down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
@@ -937,8 +993,12 @@ class StepEngine:
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
-            self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
-                       aux=D[f"a{i}"], bias=False)
+            if self._abits(i):
+                self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1],
+                           L.CONV_MASK | L.CONV_AUX_BITS, aux=D[f"ab{i}"], bias=False)
+            else:
+                self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
+                           aux=D[f"a{i}"], bias=False)
             self._wgrad("D", f"a{i}", t, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1], d[i + 1])
             if self._dbits(i):
                 # tangent through conv b, lrelu' (bits) and the avg pool in one launch; the

@@ -134,6 +134,9 @@ class CpuOps:
                 else:
                     y2[..., :cout] = z
             z = F.avg_pool2d(z.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1) * 4.0
+        elif (flags & CONV_Y2_BITS) and y2 is not None:   # unpooled: bits of the activation
+            y2[...] = 0
+            y2[..., :(cout + 7) // 8] = packbits(z > 0)
         z = z * out_scale
         if flags & CONV_PNBWD:      # PixelNorm + LReLU backward: aux = y, y2 = r
             yv = aux[..., :cout].float()
@@ -229,15 +232,20 @@ class CpuOps:
         iv = F.avg_pool2d(img, 2) if down else img
         return iv.permute(0, 2, 3, 1)
 
-    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None):
+    def from_rgb(self, img, w, b, c, y, *, B, R, C, down, slope=0.2, mask_y=None, ybits=None,
+                 mask_bits=None):
         a = self._img_in(img, down) @ w.view(C, 3).t()
         if b is not None:
             a = a + b
         a = c * a
-        if mask_y is not None:
+        if mask_bits is not None:
+            a = a * bmask(mask_bits, C, slope)
+        elif mask_y is not None:
             a = a * lmask(mask_y[..., :C], slope)
         else:
             a = F.leaky_relu(a, slope)
+            if ybits is not None:
+                ybits[...] = packbits(a > 0)
         y[..., :C] = a
 
     def from_rgb_bwd(self, gz, w, c, *, B, R, C, down, img=None, gimg=None, dw=None, db=None,

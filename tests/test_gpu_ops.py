@@ -7,6 +7,7 @@ import pytest
 import torch
 
 from cpu_ops import CpuOps, cinp, r16
+from cpu_ops import packbits as cpu_packbits
 from golden_utils import rel_l2
 
 pytestmark = pytest.mark.gpu
@@ -81,6 +82,9 @@ CONV_CASES = [
     (4, 256, 32, 64, ("bias", "lrelu", "pool")),
     (2, 256, 64, 128, ("mask", "accum")),
     (4, 256, 64, 64, ("bias", "lrelu")),
+    # the generator's input gradient through its 512^2 conv a (32 -> 64, pooled): the
+    # persistent tile 14 with compile-time flags (conv_hr_t14ef)
+    (2, 256, 32, 64, ("pool",)),
 ]
 
 
@@ -681,6 +685,111 @@ def test_sign_bit_conv_paths(B, H, c1, c2):
     assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
     for k in ("p", "tp", "gza", "dw", "db"):
         cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
+
+
+@pytest.mark.parametrize("C,R", [(16, 256), (32, 128), (16, 1024)])
+def test_from_rgb_sign_bits(C, R):
+    """pg_from_rgb_bits (bf16): the forward writes the lrelu sign bits of its output with the
+    same y as pg_from_rgb, and the tangent masked by those bits equals the tangent masked by
+    the bf16 activation (mask_y) bit for bit, and the CPU double."""
+    hip, cpu = ops_pair(torch.bfloat16)
+    B = 2
+    img = rnd(B, 3, R, R, seed=71)
+    tin = rnd(B, 3, R, R, seed=72)
+    fw, fb = rnd(C, 3, 1, 1, seed=73), rnd(C, seed=74)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = torch.bfloat16 if dev == "cuda" else torch.float32
+        r = {}
+        y = torch.zeros(B, R, R, C, dtype=dt, device=dev)
+        yb = torch.zeros(B, R, R, C // 8, dtype=torch.uint8, device=dev)
+        ops.from_rgb(img.to(dev), fw.to(dev), fb.to(dev), 0.8, y, B=B, R=R, C=C, down=False,
+                     ybits=yb)
+        r["y"], r["yb"] = y, yb
+        t = torch.zeros_like(y)
+        ops.from_rgb(tin.to(dev), fw.to(dev), None, 0.8, t, B=B, R=R, C=C, down=False,
+                     mask_bits=yb)
+        r["t"] = t
+        if dev == "cuda":
+            y0 = torch.zeros_like(y)
+            ops.from_rgb(img.to(dev), fw.to(dev), fb.to(dev), 0.8, y0, B=B, R=R, C=C, down=False)
+            assert torch.equal(y0, y)
+            assert torch.equal(yb.cpu(), cpu_packbits(y.float().cpu() > 0))
+            t0 = torch.zeros_like(y)
+            ops.from_rgb(tin.to(dev), fw.to(dev), None, 0.8, t0, B=B, R=R, C=C, down=False,
+                         mask_y=y)
+            assert torch.equal(t0, t)
+        res[dev] = r
+    cmp(res["cuda"]["y"], res["cpu"]["y"], 2e-2, "y")
+    cmp(res["cuda"]["t"], res["cpu"]["t"], 2e-2, "t")
+
+
+@pytest.mark.parametrize("B,H,c1,c2", [(1, 256, 16, 32), (1, 512, 32, 64), (1, 1024, 16, 32)])
+def test_sign_bit_mask_paths(B, H, c1, c2):
+    """bf16 lrelu' masks from sign bits (include/pggan_hip.h PG_CONV_*_BITS) for the D conv a
+    chain: the forward writes the bits of its activation (Y2_BITS, no pool), the R1 tangent
+    masks with them (AUX_BITS|MASK) and the conv-b input gradient masks its result with them
+    while reading its input through X_BITS (X_BITS|AUX_BITS|UPS_IN|MASK), against the CPU
+    double on the same bf16 data and bits, and against the bf16-activation mask on the GPU."""
+    from cpu_ops import (CONV_AUX_BITS, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_UPS_IN,
+                         CONV_X_BITS, CONV_Y2_BITS)
+    hip, cpu = ops_pair(torch.bfloat16)
+    dt = torch.bfloat16
+    for fl, ci, co in ((CONV_BIAS | CONV_LRELU | CONV_Y2_BITS, c1, c1),
+                       (CONV_MASK | CONV_AUX_BITS, c1, c1),
+                       (CONV_MASK | CONV_UPS_IN | CONV_X_BITS | CONV_AUX_BITS, c2, c1)):
+        assert hip.conv_supported(B=B, H=H, W=H, cin=ci, cout=co, flags=fl), (fl, ci, co)
+    x = q(rnd(B, H, H, c1, seed=91), dt)
+    wa = q(rnd(r16(c1) * 9 * cinp(c1), seed=92, scale=0.05), dt)
+    wd = q(rnd(r16(c1) * 9 * cinp(c2), seed=93, scale=0.05), dt)
+    bias = rnd(c1, seed=94, scale=0.1)
+    g = q(rnd(B, H // 2, H // 2, c2, seed=95), dt)
+    bb = torch.randint(0, 256, (B, H, H, c2 // 8), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(96))
+    res = {}
+    shared = None
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        d_ = dt if dev == "cuda" else torch.float32
+        X, WA, WD, BS, G = (x.to(dev).to(d_), wa.to(dev).to(d_), wd.to(dev).to(d_),
+                            bias.to(dev), g.to(dev).to(d_))
+        r = {}
+        a = torch.zeros(B, H, H, c1, dtype=d_, device=dev)
+        ab = torch.zeros(B, H, H, c1 // 8, dtype=torch.uint8, device=dev)
+        ops.conv3x3(X, WA, a, B=B, H=H, W=H, cin=c1, cout=c1,
+                    flags=CONV_BIAS | CONV_LRELU | CONV_Y2_BITS, bias=BS, y2=ab)
+        r["a"], r["ab"] = a, ab.clone()
+        if shared is None:
+            shared = (ab.cpu(), a.cpu())
+        ab, am = shared[0].to(dev), shared[1].to(dev).to(d_)     # identical operands both sides
+        ta = torch.zeros_like(a)
+        ops.conv3x3(X, WA, ta, B=B, H=H, W=H, cin=c1, cout=c1, flags=CONV_MASK | CONV_AUX_BITS,
+                    aux=ab)
+        r["ta"] = ta
+        gza = torch.zeros_like(a)
+        ops.conv3x3(G, WD, gza, B=B, H=H, W=H, cin=c2, cout=c1,
+                    flags=CONV_MASK | CONV_UPS_IN | CONV_X_BITS | CONV_AUX_BITS, aux=ab,
+                    xbits=bb.to(dev), out_scale=0.25)
+        r["gza"] = gza
+        if dev == "cuda":
+            # the same launches with the bf16 activation as the mask operand
+            ta2, gza2 = torch.zeros_like(a), torch.zeros_like(a)
+            ops.conv3x3(X, WA, ta2, B=B, H=H, W=H, cin=c1, cout=c1, flags=CONV_MASK, aux=am)
+            ops.conv3x3(G, WD, gza2, B=B, H=H, W=H, cin=c2, cout=c1,
+                        flags=CONV_MASK | CONV_UPS_IN | CONV_X_BITS, aux=am, xbits=bb.to(dev),
+                        out_scale=0.25)
+            same = (ab.cpu() == cpu_packbits(am.float().cpu() > 0)).all().item()
+            r["eq_ta"] = (ta2, same)
+            r["eq_gza"] = (gza2, same)
+        res[dev] = r
+    hb, cb = res["cuda"]["ab"].cpu(), res["cpu"]["ab"]
+    diff = (hb ^ cb).count_nonzero().item()
+    assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
+    for k in ("a", "ta", "gza"):
+        cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
+    for k in ("ta", "gza"):
+        alt, same = res["cuda"]["eq_" + k]
+        if same:    # bits == sign of the stored bf16 activation: bitwise the same result
+            assert torch.equal(alt.cpu(), res["cuda"][k].cpu()), k
 
 
 @pytest.mark.parametrize("B,H,C", [(2, 32, 16), (2, 64, 32), (2, 256, 16), (1, 512, 32)])
