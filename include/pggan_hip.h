@@ -161,6 +161,11 @@ int pg_pixnorm_lrelu_bwd_y(int dtype, int npix, int C, int cs, const void* y, co
 int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
                    const void* y, float scale, float slope, int ups, int out_cs, void* out,
                    void* stream);
+/* pg_unpool_mask (bf16, C % 8 == 0) with the lrelu' operand as sign bits, uint8 [B][H][W][C / 8]
+ * (PG_CONV_Y2_BITS of the pooled conv that produced it) instead of the bf16 activation y */
+int pg_unpool_mask_bits(int dtype, int B, int H, int W, int C, int g_cs, const void* g,
+                        const void* bits, float scale, float slope, int ups, int out_cs, void* out,
+                        void* stream);
 /* 2x2 average pool (lib/utils.py:120-124), input B x H x W */
 int pg_avgpool2(int dtype, int B, int H, int W, int C, int x_cs, const void* x, int y_cs, void* y,
                 void* stream);

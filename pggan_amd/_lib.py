@@ -106,6 +106,7 @@ _SIGS = {
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd_y": ([_I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _VP], _I),
     "pg_unpool_mask": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _F, _F, _I, _I, _VP, _VP], _I),
+    "pg_unpool_mask_bits": ([_I, _I, _I, _I, _I, _I, _VP, _VP, _F, _F, _I, _I, _VP, _VP], _I),
     "pg_avgpool2": ([_I, _I, _I, _I, _I, _I, _VP, _I, _VP, _VP], _I),
     "pg_blend": ([_I, _SZ, _F, _VP, _F, _VP, _VP, _VP], _I),
     "pg_rgb_out": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _I, _I, _VP, _VP, _VP, _F, _F, _VP,
@@ -380,8 +381,15 @@ class HipOps:
                   "pixnorm_lrelu_bwd_y")
 
     # -- elementwise -------------------------------------------------------
-    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):
-        self._cuda(g, y, out)
+    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups, bits=None):
+        """bits: the lrelu' operand as sign bits (uint8 [B, H, W, C / 8]) instead of y."""
+        self._cuda(g, y, out, bits)
+        if bits is not None:
+            self._chk(self.lib.pg_unpool_mask_bits(self._dt(out), B, H, W, C, g.shape[-1], _p(g),
+                                                   _p(bits), scale, slope, 1 if ups else 0,
+                                                   out.shape[-1], _p(out), self._s()),
+                      "unpool_mask_bits")
+            return
         self._chk(self.lib.pg_unpool_mask(self._dt(out), B, H, W, C, g.shape[-1], _p(g),
                                           y.shape[-1] if y is not None else 0, _p(y), scale, slope,
                                           1 if ups else 0, out.shape[-1], _p(out), self._s()),

@@ -1790,8 +1790,8 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
                "conv3x3_fwd: MASK flag without aux");
   PG_CHECK_ARG(!(d->flags & PG_CONV_Y2_BITS) || (y2 && d->y2_cs * 8 >= d->cout && d->y2_cs % 2 == 0),
                "conv3x3_fwd: Y2_BITS needs y2 with >= cout/8 bytes per pixel");
-  PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM | PG_CONV_PNBWD)),
-               "conv3x3_fwd: y2 only with POOL, PIXNORM or PNBWD");
+  PG_CHECK_ARG(!y2 || (d->flags & (PG_CONV_POOL | PG_CONV_PIXNORM | PG_CONV_PNBWD | PG_CONV_Y2_BITS)),
+               "conv3x3_fwd: y2 only with POOL, PIXNORM, PNBWD or Y2_BITS");
   PG_CHECK_ARG(!(d->flags & PG_CONV_PNBWD) || (aux && y2 && d->aux_cs >= d->cout && d->aux_cs % 4 == 0),
                "conv3x3_fwd: PNBWD needs aux = y (aux_cs >= cout) and y2 = r");
   PG_CHECK_ARG(dtype == PG_F32 || dtype == PG_BF16, "conv3x3_fwd: bad dtype");

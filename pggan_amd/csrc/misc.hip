@@ -1269,6 +1269,22 @@ int pg_pixnorm_lrelu_bwd_y(int dtype, int npix, int C, int cs, const void* y, co
   return PG_OK;
 }
 
+int pg_unpool_mask_bits(int dtype, int B, int H, int W, int C, int g_cs, const void* g,
+                        const void* bits, float scale, float slope, int ups, int out_cs, void* out,
+                        void* stream) {
+  PG_CHECK_ARG(dtype == PG_BF16 && g && bits && out && C % 8 == 0 &&
+                   (!ups || (H % 2 == 0 && W % 2 == 0)),
+               "unpool_mask_bits: bad args (bf16, C %% 8 == 0)");
+  if (try_unpool_mask<bf16_t>(B, H, W, C, g_cs, (const bf16_t*)g, 0, nullptr, scale, slope, ups,
+                              out_cs, (bf16_t*)out, (hipStream_t)stream,
+                              (const uint8_t*)bits) != 0) {
+    pg_set_error("unpool_mask_bits: unsupported layout (C %d, strides %d / %d)", C, g_cs, out_cs);
+    return PG_ERR_ARG;
+  }
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
 int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* g, int y_cs,
                    const void* y, float scale, float slope, int ups, int out_cs, void* out,
                    void* stream) {

@@ -581,17 +581,42 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
+    def _ubits(self, i):
+        """Below the sign-bit resolution (_dbits false): D level i's conv b still keeps its
+        pre-pool lrelu sign as bits instead of the bf16 activation where the pooled conv
+        supports it (the wide LDS-DMA tile at 64^2-256^2): the input-gradient pass forms
+        gzb = up2(g) * lrelu'(bits) in the unpool pass (pg_unpool_mask_bits), the R1 tangent
+        masks and pools in its conv (no avgpool launch); gzb itself stays materialised for the
+        input-gradient conv and the weight gradient.  PG_UBITS=0: off (A/B runs)."""
+        key = ("ubits", i, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            d, Ri, B = self.depths, 8 * 2 ** i, self.B
+            ok = bool(f is not None and self.fuse_dbits and not self._dbits(i) and
+                      os.environ.get("PG_UBITS", "1") != "0" and d[i] % 16 == 0)
+            if ok:
+                ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
+                        flags=L.CONV_BIAS | L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS)
+                      and f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
+                            flags=L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_POOL))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _abits(self, i):
         """Whether D level i's conv a also writes the sign bits of its activation (Y2_BITS
         without the pool) and the two launches that mask with lrelu'(a) -- the conv-b input
         gradient and the R1 tangent of conv a -- read those bits instead of the bf16
         activation: 16x fewer mask bytes (the 1024^2 16-channel mask is 134 MB at B = 4).
-        Only at the sign-bit levels (_dbits).  PG_ABITS=0: off (A/B runs)."""
+        Only at the sign-bit levels (_dbits).  Opt-in (PG_ABITS=1): the masks get cheaper
+        (kbench 1024^2 16->16 74.8 -> 60.5 us, the X_BITS input gradient unchanged) but writing
+        the bits costs the forward conv more (53.2 -> 66.3 us at 1024^2, 34.0 -> 42.8 at
+        512^2), and the step measured 341.7 img/s without vs 338.5 with
+        (profiles/r4_bits_ab.txt)."""
         key = ("abits", i, 0, 0, 0)
         if key not in self._ws_cache:
             f = getattr(self.ops, "conv_supported", None)
             d, Ri, B = self.depths, 8 * 2 ** i, self.B
-            ok = bool(self._dbits(i) and os.environ.get("PG_ABITS", "1") != "0" and
+            ok = bool(self._dbits(i) and os.environ.get("PG_ABITS", "0") == "1" and
                       d[i + 1] % 16 == 0)
             if ok:
                 ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i + 1],
@@ -794,6 +819,10 @@ class StepEngine:
                 self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
                            L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS, y2=D[f"mb{i}"],
                            out_scale=0.25)
+            elif self._ubits(i):
+                self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS, y2=D[f"mb{i}"],
+                           out_scale=0.25)
             else:
                 self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
                            L.CONV_LRELU | L.CONV_POOL, y2=D[f"bf{i}"], out_scale=0.25)
@@ -889,8 +918,12 @@ class StepEngine:
                            aux=D[f"ab{i}"] if ab else D[f"a{i}"],
                            dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
             else:
-                ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
-                                slope=SLOPE, ups=True)
+                if self._ubits(i):
+                    ops.unpool_mask(g, None, D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
+                                    slope=SLOPE, ups=True, bits=D[f"mb{i}"])
+                else:
+                    ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
+                                    slope=SLOPE, ups=True)
                 if GR is not None:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
                                 d[i + 1], d[i], db=GR[b + "bias"])
@@ -1009,6 +1042,13 @@ class StepEngine:
                 gb1 = D["gh"] if i == 0 else D[f"ghin{i - 1}"]
                 self._wgrad("D", f"b{i}", D[f"ta{i}"], gb1, GR[b + "weight"], Ri, d[i + 1], d[i],
                             gzbits=D[f"mb{i}"], gscale=0.25 * (alpha if i == s - 1 else 1.0))
+            elif self._ubits(i):
+                # mask (bits) and pool in the conv; the weight term reads B1's materialised gzb
+                self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tp{i}"], Ri, d[i + 1], d[i],
+                           L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_POOL, aux=D[f"mb{i}"],
+                           bias=False, out_scale=0.25)
+                self._wgrad("D", f"b{i}", D[f"ta{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
+                            d[i + 1], d[i])
             else:
                 self._conv("D", f"b{i}", D[f"ta{i}"], D[f"tbf{i}"], Ri, d[i + 1], d[i],
                            L.CONV_MASK, aux=D[f"bf{i}"], bias=False)

@@ -186,12 +186,14 @@ class CpuOps:
         gz[..., :C] = rr * (b - a * (a * b).mean(-1, keepdim=True)) * lmask(a, slope)
 
     # -- elementwise -------------------------------------------------------
-    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups):
+    def unpool_mask(self, g, y, out, *, B, H, W, C, scale, slope, ups, bits=None):
         v = g[..., :C]
         if ups:
             v = v.repeat_interleave(2, 1).repeat_interleave(2, 2)
         v = v * scale
-        if y is not None:
+        if bits is not None:
+            v = v * bmask(bits, C, slope)
+        elif y is not None:
             v = v * lmask(y[..., :C], slope)
         out[..., :C] = v
 

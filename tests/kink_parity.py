@@ -56,7 +56,7 @@ def d_masks(eng):
         m["rgbd"] = _nchw(D["yd"], d[s - 1]) > 0 if eng._last_dlow else None
     for i in range(s):
         m[f"a{i}"] = _nchw(D[f"a{i}"], d[i + 1]) > 0
-        if eng._dbits(i):
+        if eng._dbits(i) or eng._ubits(i):
             m[f"b{i}"] = _unpack_bits(D[f"mb{i}"], d[i])
         else:
             m[f"b{i}"] = _nchw(D[f"bf{i}"], d[i]) > 0

@@ -27,7 +27,9 @@ def build(meta, ops, device="cpu"):
                        {k: torch.from_numpy(v) for k, v in PD.items()})
     eng = E.StepEngine(ops, depths, s, B, device)
     if device == "cpu":
-        eng.dbits_min_res = 8      # exercise the sign-bit schedule at the fixture sizes
+        # exercise both sign-bit schedules at the fixture sizes: 8^2 keeps the conv-b bits for
+        # the unpool pass (_ubits), >= 16^2 the full sign-bit path (_dbits)
+        eng.dbits_min_res = 16
     eng.bind(fpG, fpD, E.Hyper())
     eng.keep_fake_D = True
     return eng, fpG, fpD

@@ -82,8 +82,7 @@ CONV_CASES = [
     (4, 256, 32, 64, ("bias", "lrelu", "pool")),
     (2, 256, 64, 128, ("mask", "accum")),
     (4, 256, 64, 64, ("bias", "lrelu")),
-    # the generator's input gradient through its 512^2 conv a (32 -> 64, pooled): the
-    # persistent tile 14 with compile-time flags (conv_hr_t14ef)
+    # the generator's input gradient through its 512^2 conv a (32 -> 64, pooled)
     (2, 256, 32, 64, ("pool",)),
 ]
 
@@ -684,6 +683,60 @@ def test_sign_bit_conv_paths(B, H, c1, c2):
     diff = (hb ^ cb).count_nonzero().item()
     assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
     for k in ("p", "tp", "gza", "dw", "db"):
+        cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
+
+
+@pytest.mark.parametrize("B,H,c1,c2", [(2, 128, 128, 256), (4, 64, 256, 512), (1, 256, 64, 128)])
+def test_sign_bit_unpool_paths(B, H, c1, c2):
+    """The conv-b sign bits below the full sign-bit resolution (engine._ubits, the wide LDS-DMA
+    tile): forward with Y2_BITS|POOL, the R1 tangent with AUX_BITS|MASK|POOL against the CPU
+    double, and the unpool pass reading the bits (pg_unpool_mask_bits) bitwise equal to the
+    same pass reading the bf16 activation whose signs they are."""
+    from cpu_ops import CONV_AUX_BITS, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_Y2_BITS
+    hip, cpu = ops_pair(torch.bfloat16)
+    dt = torch.bfloat16
+    for fl in (CONV_BIAS | CONV_LRELU | CONV_POOL | CONV_Y2_BITS, CONV_MASK | CONV_AUX_BITS | CONV_POOL):
+        assert hip.conv_supported(B=B, H=H, W=H, cin=c1, cout=c2, flags=fl), fl
+    a = q(rnd(B, H, H, c1, seed=101), dt)
+    wf = q(rnd(r16(c2) * 9 * cinp(c1), seed=102, scale=0.05), dt)
+    bias = rnd(c2, seed=103, scale=0.1)
+    g = q(rnd(B, H // 2, H // 2, c2, seed=104), dt)
+    res, shared = {}, None
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        d_ = dt if dev == "cuda" else torch.float32
+        A, WF, BS, G = a.to(dev).to(d_), wf.to(dev).to(d_), bias.to(dev), g.to(dev).to(d_)
+        r = {}
+        p = torch.zeros(B, H // 2, H // 2, c2, dtype=d_, device=dev)
+        bits = torch.zeros(B, H, H, c2 // 8, dtype=torch.uint8, device=dev)
+        ops.conv3x3(A, WF, p, B=B, H=H, W=H, cin=c1, cout=c2,
+                    flags=CONV_BIAS | CONV_LRELU | CONV_POOL | CONV_Y2_BITS, bias=BS, y2=bits,
+                    out_scale=0.25)
+        r["p"], r["bits"] = p, bits.clone()
+        if shared is None:
+            shared = bits.cpu()
+        bits = shared.to(dev)
+        tp = torch.zeros_like(p)
+        ops.conv3x3(A, WF, tp, B=B, H=H, W=H, cin=c1, cout=c2,
+                    flags=CONV_MASK | CONV_AUX_BITS | CONV_POOL, aux=bits, out_scale=0.25)
+        r["tp"] = tp
+        gz = torch.zeros(B, H, H, c2, dtype=d_, device=dev)
+        ops.unpool_mask(G, None, gz, B=B, H=H, W=H, C=c2, scale=0.25, slope=0.2, ups=True,
+                        bits=bits)
+        r["gz"] = gz
+        if dev == "cuda":
+            # the bf16 pre-pool activation with exactly these signs -> the same unpool result
+            y2 = torch.zeros(B, H, H, c2, dtype=d_, device=dev)
+            ops.conv3x3(A, WF, torch.zeros_like(p), B=B, H=H, W=H, cin=c1, cout=c2,
+                        flags=CONV_BIAS | CONV_LRELU | CONV_POOL, bias=BS, y2=y2, out_scale=0.25)
+            if torch.equal(cpu_packbits(y2.float().cpu() > 0), shared):
+                gz2 = torch.zeros_like(gz)
+                ops.unpool_mask(G, y2, gz2, B=B, H=H, W=H, C=c2, scale=0.25, slope=0.2, ups=True)
+                assert torch.equal(gz2, gz)
+        res[dev] = r
+    hb, cb = res["cuda"]["bits"].cpu(), res["cpu"]["bits"]
+    diff = (hb ^ cb).count_nonzero().item()
+    assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
+    for k in ("p", "tp", "gz"):
         cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
 
 
