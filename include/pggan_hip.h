@@ -346,8 +346,9 @@ int pg_augment_u8(int B, int H, int W, const void* src, const float* params, flo
  * torch's cross-stream events record with a system-scope release: every record writes back and
  * invalidates the L2 of all XCDs and the next kernel on that stream starts ~6.5 us late.  The
  * two streams are on one device, so these events release to device scope only
- * (hipEventReleaseToDevice).  `timing` != 0: a timing event that also skips the system fence
- * (hipEventDisableSystemFence), for the bench's per-launch timers.  Handles are opaque. */
+ * (hipEventReleaseToDevice).  `timing` != 0: a timing event that skips the system fence
+ * (hipEventDisableSystemFence; a default timing event where the runtime rejects that flag), for
+ * the bench's per-launch timers.  Handles are opaque. */
 int pg_event_create(int timing, void** ev);
 int pg_event_record(void* ev, void* stream);
 int pg_stream_wait_event(void* stream, void* ev);

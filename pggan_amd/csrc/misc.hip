@@ -1856,10 +1856,18 @@ static int pg_hip_status(hipError_t e, const char* what) {
 
 int pg_event_create(int timing, void** ev) {
   PG_CHECK_ARG(ev, "event_create: null out");
-  const unsigned flags = timing ? (hipEventDisableSystemFence | hipEventReleaseToDevice)
+  // timing events: HIP rejects hipEventReleaseToDevice beside hipEventDisableSystemFence
+  // (invalid argument on ROCm 7.2), so the timing form skips the fence only; a runtime that
+  // rejects that too gets a default timing event
+  const unsigned flags = timing ? hipEventDisableSystemFence
                                 : (hipEventDisableTiming | hipEventReleaseToDevice);
   hipEvent_t e = nullptr;
-  const int rc = pg_hip_status(hipEventCreateWithFlags(&e, flags), "hipEventCreateWithFlags");
+  hipError_t err = hipEventCreateWithFlags(&e, flags);
+  if (err != hipSuccess && timing) {
+    (void)hipGetLastError();
+    err = hipEventCreateWithFlags(&e, hipEventDefault);
+  }
+  const int rc = pg_hip_status(err, "hipEventCreateWithFlags");
   *ev = rc == PG_OK ? (void*)e : nullptr;
   return rc;
 }
