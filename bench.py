@@ -104,7 +104,10 @@ class KernelTimer:
         if os.environ.get("PG_TORCH_EVENTS", "0") == "1":
             self.ev = lambda: torch.cuda.Event(enable_timing=True)
         else:
-            self.ev = lambda: ops.event(timing=True)
+            # created here, before any timed step: ~0.5k events per instrumented step, and
+            # creating them inside the step made the host the bottleneck of that step
+            pool = [ops.event(timing=True) for _ in range(2048)]
+            self.ev = lambda: pool.pop() if pool else ops.event(timing=True)
 
         def conv3x3(x, wpk, y, **kw):
             if not self.on:

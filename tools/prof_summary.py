@@ -5,7 +5,8 @@
                                  [-o out.json]
 
 Families (same bracketing as bench.py's HIP events):
-  conv3x3  = conv3x3_kernel dispatches + their split-K epilogue dispatches, per conv call
+  conv3x3  = conv3x3_kernel / conv_hr_kernel / conv_lr_kernel / conv_kg_kernel dispatches + their
+             split-K epilogue dispatches, per conv call
   wgrad3x3 = wgrad3x3_kernel / wgrad_bf16_kernel / wgrad_dma_kernel dispatches (bias grad fused), per call
 Traffic per call = 2 * FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md "HBM [CDNA4]": gfx950
 FETCH_SIZE reports half of the bytes of wide coalesced reads; WRITE_SIZE is exact for
@@ -20,7 +21,8 @@ from collections import defaultdict
 
 
 def family(name):
-    if "conv3x3_kernel" in name or "conv_hr_kernel" in name or "conv_lr_kernel" in name:
+    if ("conv3x3_kernel" in name or "conv_hr_kernel" in name or "conv_lr_kernel" in name or
+            "conv_kg_kernel" in name):
         return "conv3x3", True
     if "conv_splitk_epilogue" in name:
         return "conv3x3", False
