@@ -187,6 +187,13 @@ int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, cons
 /* fromRGB: y = lrelu(c*(W . img_in + b)), img_in = down ? avgpool2(img) : img  (img NCHW fp32);
  * R = output resolution.  b == NULL -> no bias; mask_y != NULL -> tangent mode:
  * y = c*(W . img_in) * lrelu'(mask_y) (no activation) */
+/* the toRGB input gradient fused with the PixelNorm + LReLU backward of its input y (the level's
+ * PG_CONV_PIXNORM output, r its per-pixel factor fp32 [B*R*R]): gz = r (v - y mean_c(y v))
+ * lrelu'(y), v = c W^T gimg (pg_rgb_out_bwd's gx then pg_pixnorm_lrelu_bwd_y, without v's round
+ * trip through HBM); C 16 or 32, alpha = 1 (no fade-in branch) */
+int pg_rgb_out_bwd_pn(int dtype, int B, int R, int C, int y_cs, const void* y, const float* r,
+                      const float* w, float c, const float* gimg, float slope, int gz_cs, void* gz,
+                      void* stream);
 int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
                 const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
                 void* stream);

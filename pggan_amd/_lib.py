@@ -118,6 +118,7 @@ _SIGS = {
     "pg_img_fade": ([_I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_from_rgb_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP, _I,
                          _VP, _VP], _I),
+    "pg_rgb_out_bwd_pn": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _F, _I, _VP, _VP], _I),
     "pg_from_rgb_bits": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP,
                           _I, _VP, _VP, _VP], _I),
     "pg_from_rgb_bwd_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _F, _I, _VP, _VP,
@@ -420,6 +421,13 @@ class HipOps:
                                           xp.shape[-1] if xp is not None else 0, _p(xp), _p(wp), cp,
                                           alpha, _p(gimg), _p(gx), _p(gxp), _p(dw), _p(db), _p(dwp),
                                           _p(dbp), self._s()), "rgb_out_bwd")
+
+    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope):
+        """toRGB input gradient + the PixelNorm / LReLU backward of its input y (pg_rgb_out_bwd_pn)."""
+        self._cuda(y, r, w, gimg, gz)
+        self._chk(self.lib.pg_rgb_out_bwd_pn(self._dt(y), B, R, C, y.shape[-1], _p(y), _p(r), _p(w), c,
+                                             _p(gimg), slope, gz.shape[-1], _p(gz), self._s()),
+                  "rgb_out_bwd_pn")
 
     def _src(self, img):
         """pg_img_src of an image operand (a tensor or an ImgMix)."""

@@ -474,8 +474,11 @@ int launch_kg(const pg_conv_desc* d, const void* x, const void* wpk, const float
 // pooling; at 128^2 and for the pooled 64^2 layers conv_hr's tiles are as fast or faster; the
 // one- / two-chunk layers at >= 256^2 run one workgroup per CU with everything exposed in
 // conv_hr, which the one-slot form overlaps.
+// Whole-step A/B (profiles/r4_kg_ab.txt): neutral at C5 (350.7 vs 350.2 img/s with / without),
+// slower at C3 (475.3 vs 480.9) and C4's shard (541.5 vs 548.3), so it is opt-in (PG_KG=1).
 int kg_variant(const pg_conv_desc* d) {
-  static const int mode = getenv("PG_KG") ? atoi(getenv("PG_KG")) : 1;
+  const char* env = getenv("PG_KG");   // read per call: the op tests switch it within a process
+  const int mode = env ? atoi(env) : 0;
   if (!mode) return 0;
   const int cin_p = (d->cin + 31) & ~31;
   const bool pool = (d->flags & PG_CONV_POOL) != 0;
@@ -487,7 +490,8 @@ int kg_variant(const pg_conv_desc* d) {
 }
 }  // namespace
 
-// Whether conv_kg takes this bf16 conv (PG_KG=0: never; 2: every eligible shape; A/B runs).
+// Whether conv_kg takes this bf16 conv (PG_KG=0, the default: never; 1: the shapes kg_variant
+// picks; 2: every eligible shape; A/B runs).
 bool conv_kg_ok(const pg_conv_desc* d) {
   const int v = kg_variant(d);
   if (!v) return false;

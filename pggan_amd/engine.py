@@ -750,14 +750,31 @@ class StepEngine:
                       alpha=alpha, gxp=g[f"gy{s - 1}"], dwp=GR[pre + "weight"],
                       dbp=GR[pre + "bias"])
         pre = f"toRGB_blocks.{s}.toRGB.module."
-        ops.rgb_out_bwd(self._ylvl(s), P[pre + "weight"], he(d[s]), gimg, g[f"gy{s}"],
-                        GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s], **kw)
+        # the toRGB input gradient with the top block's PixelNorm backward fused in
+        # (pg_rgb_out_bwd_pn: the 16-channel 1024^2 dL/dy never goes through HBM); its weight
+        # gradient on the side stream
+        top_pn = (s >= 1 and not low and hasattr(ops, "rgb_out_bwd_pn") and d[s] in (16, 32) and
+                  os.environ.get("PG_RGB_PNBWD", "1") != "0" and
+                  self._pn_fused(self.R, d[s], d[s], L.CONV_LRELU))
+        w_rgb = P[pre + "weight"]
+        if top_pn:
+            ops.rgb_out_bwd_pn(self._ylvl(s), g[f"rb{s - 1}"], w_rgb, he(d[s]), gimg,
+                               g[f"gzb{s - 1}"], B=B, R=self.R, C=d[s], slope=SLOPE)
+        else:
+            ops.rgb_out_bwd(self._ylvl(s), w_rgb, he(d[s]), gimg, g[f"gy{s}"], None, None,
+                            B=B, R=self.R, C=d[s],
+                            **{k: (None if k in ("dwp", "dbp") else v) for k, v in kw.items()})
+        # img / the fade-in branch's operands are D / G buffers: pending for both nets
+        self._side_call(("G", "D"), ops.rgb_out_bwd, self._ylvl(s), w_rgb, he(d[s]), gimg, None,
+                        GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s],
+                        **{k: (None if k == "gxp" else v) for k, v in kw.items()})
         self._ready("G", pre, *([f"toRGB_blocks.{s - 1}.toRGB.module."] if s >= 1 else []))
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
-            self._g_pn_bwd(f"b{i}", g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], g[f"gy{i + 1}"],
-                           g[f"gzb{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
+            if not (top_pn and i == s - 1):
+                self._g_pn_bwd(f"b{i}", g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], g[f"gy{i + 1}"],
+                               g[f"gzb{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
                         d[i + 1],
                         db=GR[b + "bias"])

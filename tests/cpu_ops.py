@@ -217,16 +217,26 @@ class CpuOps:
                     alpha=1.0, gxp=None, dwp=None, dbp=None):
         fa = alpha * c if xp is not None else c
         g = gimg.permute(0, 2, 3, 1)
-        gx[..., :C] = fa * g @ w.view(3, C)
-        dw.view(3, C).add_(fa * torch.einsum("bhwo,bhwk->ok", g, x[..., :C]))
-        db.add_(fa * g.reshape(-1, 3).sum(0))
+        if gx is not None:
+            gx[..., :C] = fa * g @ w.view(3, C)
+        if dw is not None:
+            dw.view(3, C).add_(fa * torch.einsum("bhwo,bhwk->ok", g, x[..., :C]))
+        if db is not None:
+            db.add_(fa * g.reshape(-1, 3).sum(0))
         if xp is not None:
             fp = (1 - alpha) * cp
             gs = F.avg_pool2d(gimg, 2).permute(0, 2, 3, 1) * 4.0
             if gxp is not None:
                 gxp[..., :Cp] = fp * gs @ wp.view(3, Cp)
-            dwp.view(3, Cp).add_(fp * torch.einsum("bhwo,bhwk->ok", gs, xp[..., :Cp]))
-            dbp.add_(fp * gs.reshape(-1, 3).sum(0))
+            if dwp is not None:
+                dwp.view(3, Cp).add_(fp * torch.einsum("bhwo,bhwk->ok", gs, xp[..., :Cp]))
+            if dbp is not None:
+                dbp.add_(fp * gs.reshape(-1, 3).sum(0))
+
+    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope):
+        gy = torch.zeros_like(y)
+        gy[..., :C] = c * gimg.permute(0, 2, 3, 1) @ w.view(3, C)
+        self.pixnorm_lrelu_bwd_y(y, r, gy, gz, C, slope)
 
     def _img_in(self, img, down):
         if hasattr(img, "materialize"):      # pggan_amd._lib.ImgMix

@@ -449,9 +449,11 @@ KG_CASES = [
 
 
 @pytest.mark.parametrize("case", KG_CASES)
-def test_conv_kg(case):
-    """bf16 wide convs through the K-grouped kernel against the CPU double: output, the
-    pre-pool copy (y2 with POOL) and the PixelNorm factor (y2 with PIXNORM)."""
+def test_conv_kg(case, monkeypatch):
+    """bf16 wide convs through the K-grouped kernel (opt-in; PG_KG=2 takes it for every eligible
+    shape) against the CPU double: output, the pre-pool copy (y2 with POOL) and the PixelNorm
+    factor (y2 with PIXNORM)."""
+    monkeypatch.setenv("PG_KG", "2")
     B, H, cin, cout, fl = case
     _L = lib()
     dtype = torch.bfloat16
@@ -738,6 +740,34 @@ def test_sign_bit_unpool_paths(B, H, c1, c2):
     assert diff <= max(2, hb.numel() // 2000), f"{diff} bit bytes differ"
     for k in ("p", "tp", "gz"):
         cmp(res["cuda"][k], res["cpu"][k], 2e-2, f"{k} H={H} {c1}->{c2}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,R", [(16, 1024), (32, 128)])
+def test_rgb_out_bwd_pn(dtype, C, R):
+    """pg_rgb_out_bwd_pn: the toRGB input gradient with the PixelNorm + LReLU backward of its
+    input fused in, against the CPU double and against the unfused HIP pair (rgb_out_bwd ->
+    gy in the storage dtype -> pixnorm_lrelu_bwd_y)."""
+    hip, cpu = ops_pair(dtype)
+    B = 2
+    y = q(rnd(B, R, R, C, seed=111), dtype)
+    r = rnd(B * R * R, seed=112).abs() + 0.5
+    w = rnd(3, C, 1, 1, seed=113)
+    gimg = rnd(B, 3, R, R, seed=114)
+    res = {}
+    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
+        dt = dtype if dev == "cuda" else torch.float32
+        Y, Rr, Wd, G = y.to(dev).to(dt), r.to(dev), w.to(dev), gimg.to(dev)
+        gz = torch.zeros(B, R, R, C, dtype=dt, device=dev)
+        ops.rgb_out_bwd_pn(Y, Rr, Wd, 0.35, G, gz, B=B, R=R, C=C, slope=0.2)
+        res[dev] = gz
+        if dev == "cuda":
+            gy = torch.zeros_like(gz)
+            ops.rgb_out_bwd(Y, Wd, 0.35, G, gy, None, None, B=B, R=R, C=C)
+            gz2 = torch.zeros_like(gz)
+            ops.pixnorm_lrelu_bwd_y(Y, Rr, gy, gz2, C, 0.2)
+            cmp(gz, gz2.cpu(), tol_for(dtype, 1e-6), "fused vs unfused")
+    cmp(res["cuda"], res["cpu"], tol_for(dtype, 1e-6), f"gz C={C} R={R}")
 
 
 @pytest.mark.parametrize("C,R", [(16, 256), (32, 128), (16, 1024)])

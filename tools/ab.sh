@@ -7,7 +7,8 @@
 #
 # With -k every variant runs tools/kbench.py on the specs (printed: the minimum over rounds per
 # spec and variant); without it a whole-step bench.py (10 timed steps after 3 warm-up, no CPU
-# baseline; printed: img/s and ms/step per round).  Variants alternate within each round.
+# baseline, extra bench arguments from $AB_ARGS; printed: img/s and ms/step per round).
+# Variants alternate within each round.
 # Logs: gpurun_out/ab.log.  Replaces the round-2/3 one-off wrappers (*_ab.sh, *_sweep.sh).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -28,7 +29,7 @@ for i in $(seq "$rounds"); do
     else
       [ -n "$lib" ] && { cp pggan_amd/libpggan_hip.so /tmp/ab_lib_cur.so; cp "$lib" pggan_amd/libpggan_hip.so; }
       env $envs timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-baseline off --no-kernel-events \
-        > gpurun_out/ab_bench.json 2> gpurun_out/ab_bench.err
+        ${AB_ARGS:-} > gpurun_out/ab_bench.json 2> gpurun_out/ab_bench.err
       rc=$?
       [ -n "$lib" ] && cp /tmp/ab_lib_cur.so pggan_amd/libpggan_hip.so
       [ $rc -eq 0 ] || { echo "bench $name failed"; tail -5 gpurun_out/ab_bench.err; exit $rc; }
