@@ -75,8 +75,10 @@ int pg_version(void);
  * pg_conv3x3_supported): with v the conv result = dL/dy of a PG_CONV_PIXNORM output y, the
  * launch writes dL/du = r * (v - y * mean_c(y * v)) * lrelu'(y), u the pre-norm activation
  * (pg_pixnorm_lrelu_bwd_y without the round trip of v through HBM).  aux = y (storage
- * dtype, aux_cs), y2 = r (fp32 [B*H*W], from the forward).  Not with BIAS / POOL / MASK /
- * ACCUM / PIXNORM / bit flags. */
+ * dtype, aux_cs), y2 = r (fp32 [B*H*W], from the forward).  With POOL (32 output channels):
+ * applied to the pooled result, y and r at the pooled resolution (the generator's input
+ * gradient through an upsampling conv a, then the previous block's PixelNorm).  Not with
+ * BIAS / MASK / ACCUM / PIXNORM / bit flags. */
 #define PG_CONV_PNBWD 2048
 /* Channel-blocked activations: the operand is [B][C/32][H][W][32] (C = its channel stride,
  * a multiple of 32) instead of NHWC -- a 32-channel slice of a pixel row is contiguous. */

@@ -1656,8 +1656,10 @@ bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
   if (d->flags & PG_CONV_PNBWD) {   // conv_hr epilogue, [cout][pixel] tiles of <= 32 channels
     if constexpr (sizeof(T) != 2) return false;
-    if (d->flags & (BITS | PG_CONV_BIAS | PG_CONV_POOL | PG_CONV_MASK | PG_CONV_ACCUM | PG_CONV_PIXNORM))
+    if (d->flags & (BITS | PG_CONV_BIAS | PG_CONV_MASK | PG_CONV_ACCUM | PG_CONV_PIXNORM))
       return false;
+    // after a 2x2 pool: the 32-channel tiles (their swap epilogue; y and r at pooled resolution)
+    if ((d->flags & PG_CONV_POOL) && (d->cout != 32 || conv_hr_bn(d) != 32)) return false;
     return conv_hr_ok(d) && ((d->cout + 15) & ~15) <= conv_hr_bn(d) && conv_hr_bn(d) <= 32 &&
            d->cout % 4 == 0;
   }

@@ -644,6 +644,22 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
+    def _pn_pool(self, i):
+        """Whether level i's conv-a input gradient (pooled to level i-1) also applies level
+        i-1's conv-b PixelNorm + LReLU backward (PG_CONV_POOL | PG_CONV_PNBWD): level i-1's
+        forward kept y and r (fused PixelNorm) and the kernel supports it (32 channels).
+        PG_PN_POOL=0: off (A/B runs)."""
+        key = ("pnpool", i, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = getattr(self.ops, "conv_supported", None)
+            d, Ri, B = self.depths, 8 * 2 ** i, self.B
+            ok = bool(i >= 1 and f is not None and os.environ.get("PG_PN_POOL", "1") != "0" and
+                      self._pn_fused(Ri // 2, d[i], d[i], L.CONV_LRELU) and
+                      f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
+                        flags=L.CONV_POOL | L.CONV_PNBWD))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _pn_fused(self, H, cin, cout, flags):
         """Whether this generator conv can run PixelNorm in its epilogue (all output
         channels in one tile of the kernel the library picks for the shape)."""
@@ -769,10 +785,11 @@ class StepEngine:
                         GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s],
                         **{k: (None if k == "gxp" else v) for k, v in kw.items()})
         self._ready("G", pre, *([f"toRGB_blocks.{s - 1}.toRGB.module."] if s >= 1 else []))
+        pn_done = s - 1 if top_pn else None   # level whose conv-b PixelNorm backward is done
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.3.module."
-            if not (top_pn and i == s - 1):
+            if pn_done != i:
                 self._g_pn_bwd(f"b{i}", g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], g[f"gy{i + 1}"],
                                g[f"gzb{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
             self._wgrad("G", f"b{i}", g[f"ya{i}"], g[f"gzb{i}"], GR[b + "weight"], Ri, d[i + 1],
@@ -795,8 +812,15 @@ class StepEngine:
             self._ready("G", a)
             # level s-1 also received the toRGB fade-in branch's gradient: accumulate
             flags = L.CONV_POOL | (L.CONV_ACCUM if (i == s - 1 and low) else 0)
-            self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
-                       dgrad=True, out_scale=1.0)                     # up2 backward = 2x2 sum
+            if not (flags & L.CONV_ACCUM) and self._pn_pool(i):
+                # the level below's conv-b PixelNorm backward after the pool, in this launch
+                self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gzb{i - 1}"], Ri, d[i + 1], d[i],
+                           L.CONV_POOL | L.CONV_PNBWD, dgrad=True, out_scale=1.0,
+                           aux=g[f"yb{i - 1}"], y2=g[f"rb{i - 1}"])
+                pn_done = i - 1
+            else:
+                self._conv("G", f"a{i}", g[f"gza{i}"], g[f"gy{i}"], Ri, d[i + 1], d[i], flags,
+                           dgrad=True, out_scale=1.0)                 # up2 backward = 2x2 sum
         fb = "first_block.block.0.module."
         self._g_pn_bwd("first", g["u0"], g["y0"], g["r0"], g["gy0"], g["gz0"], 4, d[0], d[0],
                        L.CONV_LRELU)

@@ -127,7 +127,7 @@ class CpuOps:
         if flags & CONV_POOL:
             if (flags & CONV_MASK) and (flags & CONV_AUX_BITS):   # mask before the pool
                 z = z * bmask(aux, cout, slope)
-            if y2 is not None:
+            if y2 is not None and not (flags & CONV_PNBWD):   # PNBWD: y2 is its input r
                 if flags & CONV_Y2_BITS:
                     y2[...] = 0
                     y2[..., :(cout + 7) // 8] = packbits(z > 0)
@@ -140,7 +140,7 @@ class CpuOps:
         z = z * out_scale
         if flags & CONV_PNBWD:      # PixelNorm + LReLU backward: aux = y, y2 = r
             yv = aux[..., :cout].float()
-            r = y2.reshape(B, H, W, 1).float()
+            r = y2.reshape(z.shape[:-1] + (1,)).float()      # pooled resolution after a POOL
             z = r * (z - yv * (yv * z).mean(-1, keepdim=True)) * lmask(yv, slope)
         if (flags & CONV_MASK) and not (flags & CONV_POOL):
             z = z * (bmask(aux, cout, slope) if flags & CONV_AUX_BITS else lmask(aux[..., :cout], slope))

@@ -875,6 +875,42 @@ def test_sign_bit_mask_paths(B, H, c1, c2):
             assert torch.equal(alt.cpu(), res["cuda"][k].cpu()), k
 
 
+@pytest.mark.parametrize("B,H,cin", [(2, 64, 16), (1, 1024, 16), (2, 256, 16)])
+def test_pixnorm_bwd_after_pool(B, H, cin):
+    """PG_CONV_PNBWD | PG_CONV_POOL (bf16, 32 output channels): the generator's upsampling
+    conv-a input gradient (2x2 sum) followed by the previous block's PixelNorm + LReLU
+    backward at the pooled resolution, in one launch, against an fp32 restatement on the CPU
+    double and the unfused HIP pair (pooled conv -> gy in bf16 -> pg_pixnorm_lrelu_bwd_y)."""
+    from cpu_ops import CONV_PNBWD, CONV_POOL
+    C = 32
+    hip, cpu = ops_pair(torch.bfloat16)
+    dt = torch.bfloat16
+    fl = CONV_POOL | CONV_PNBWD
+    assert hip.conv_supported(B=B, H=H, W=H, cin=cin, cout=C, flags=fl)
+    Hp = H // 2
+    gz = q(rnd(B, H, H, cin, seed=121), dt)
+    wd = q(rnd(r16(C) * 9 * cinp(cin), seed=122, scale=0.05), dt)
+    u = rnd(B, Hp, Hp, C, seed=123)
+    r = torch.rsqrt((u * u).mean(-1) + 1e-8)
+    y = q(u * r[..., None], dt)
+    v = torch.zeros(B, Hp, Hp, C)
+    cpu.conv3x3(gz, wd, v, B=B, H=H, W=H, cin=cin, cout=C, flags=CONV_POOL, out_scale=1.0)
+    ref = r[..., None] * (v - y * (y * v).mean(-1, keepdim=True)) * torch.where(y > 0, 1.0, 0.2)
+    G, WD, Y, Rr = gz.cuda().to(dt), wd.cuda().to(dt), y.cuda().to(dt), r.cuda().contiguous()
+    out = torch.zeros(B, Hp, Hp, C, dtype=dt, device="cuda")
+    hip.conv3x3(G, WD, out, B=B, H=H, W=H, cin=cin, cout=C, flags=fl, aux=Y, y2=Rr, out_scale=1.0)
+    gy = torch.zeros(B, Hp, Hp, C, dtype=dt, device="cuda")
+    hip.conv3x3(G, WD, gy, B=B, H=H, W=H, cin=cin, cout=C, flags=CONV_POOL, out_scale=1.0)
+    unf = torch.zeros_like(gy)
+    hip.pixnorm_lrelu_bwd_y(Y, Rr, gy, unf, C, 0.2)
+    out2 = torch.zeros(B, Hp, Hp, C)
+    cpu.conv3x3(gz, wd, out2, B=B, H=H, W=H, cin=cin, cout=C, flags=fl, aux=y, y2=r, out_scale=1.0)
+    torch.cuda.synchronize()
+    cmp(out, ref, 1e-2, f"pooled PNBWD H={H}")
+    cmp(out, out2, 1e-2, f"pooled PNBWD vs CPU double H={H}")
+    cmp(out, unf.float().cpu(), 2e-2, f"fused vs unfused H={H}")
+
+
 @pytest.mark.parametrize("B,H,C", [(2, 32, 16), (2, 64, 32), (2, 256, 16), (1, 512, 32)])
 def test_pixnorm_bwd_fused_dgrad(B, H, C):
     """PG_CONV_PNBWD (bf16, include/pggan_hip.h): the input-gradient conv writes the
