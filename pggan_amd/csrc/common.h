@@ -45,6 +45,19 @@ __device__ __forceinline__ u32x4_t lrelu_mask_bf16x8(u32x4_t v, unsigned m, floa
   }
   return v;
 }
+// The same mask with the factors from a 16-entry LDS table (entry e: 4 floats, (e >> j) & 1 ?
+// 1.0 : slope): two 16-B reads per byte instead of a compare + select per element (the staging
+// of the sign-bit input-gradient tiles is VALU-bound).  Bitwise the same result.
+__device__ __forceinline__ u32x4_t lrelu_mask_bf16x8_lut(u32x4_t v, unsigned m, const char* lut) {
+  typedef __attribute__((ext_vector_type(4))) float f4_t;
+  const f4_t f0 = *reinterpret_cast<const f4_t*>(lut + ((m & 15u) << 4));
+  const f4_t f1 = *reinterpret_cast<const f4_t*>(lut + (((m >> 4) & 15u) << 4));
+  v[0] = pack_bf16x2(__uint_as_float(v[0] << 16) * f0[0], __uint_as_float(v[0] & 0xffff0000u) * f0[1]);
+  v[1] = pack_bf16x2(__uint_as_float(v[1] << 16) * f0[2], __uint_as_float(v[1] & 0xffff0000u) * f0[3]);
+  v[2] = pack_bf16x2(__uint_as_float(v[2] << 16) * f1[0], __uint_as_float(v[2] & 0xffff0000u) * f1[1]);
+  v[3] = pack_bf16x2(__uint_as_float(v[3] << 16) * f1[2], __uint_as_float(v[3] & 0xffff0000u) * f1[3]);
+  return v;
+}
 __device__ __forceinline__ bf16_t f2bf(float f) {
   const __bf16 h = (__bf16)f;
   return __builtin_bit_cast(bf16_t, h);
