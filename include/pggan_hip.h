@@ -362,6 +362,13 @@ int pg_event_create(int timing, void** ev);
 int pg_event_record(void* ev, void* stream);
 int pg_stream_wait_event(void* stream, void* ev);
 int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);
+/* Arm `ev` (NULL: disarm) for the next kernel this library launches on `stream` from this host
+ * thread: that launch records the event at its completion (hipExtLaunchKernel's stop event), with
+ * no marker packet of its own in the stream's queue -- hipEventRecord's marker delays the
+ * stream's next kernel by ~6.5 us on MI355X.  pg_event_armed() is 1 while the event still waits
+ * for its launch (then record it with pg_event_record). */
+int pg_event_arm(void* ev, void* stream);
+int pg_event_armed(void);
 int pg_event_destroy(void* ev);
 
 /* ---- step plan: the kernel path of every 3x3 conv pass (forward, input

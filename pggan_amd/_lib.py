@@ -160,6 +160,8 @@ _SIGS = {
     "pg_stream_wait_event": ([_VP, _VP], _I),
     "pg_event_elapsed_ms": ([_VP, _VP, ctypes.POINTER(ctypes.c_float)], _I),
     "pg_event_destroy": ([_VP], _I),
+    "pg_event_arm": ([_VP, _VP], _I),
+    "pg_event_armed": ([], _I),
 }
 SYMBOLS = ["pg_last_error"] + list(_SIGS)
 
@@ -211,6 +213,12 @@ class HipEvent:
         rc = self.lib.pg_stream_wait_event(ctypes.c_void_p(s.cuda_stream), self.h)
         if rc != 0:
             raise RuntimeError(f"stream_wait_event failed ({rc}): {self.lib.pg_last_error().decode()}")
+
+    def arm(self, stream=None):
+        """Record this event at the completion of the next kernel the library launches on
+        `stream` (default: current) from this thread (pg_event_arm)."""
+        s = stream if stream is not None else torch.cuda.current_stream()
+        self.lib.pg_event_arm(self.h, ctypes.c_void_p(s.cuda_stream))
 
     def elapsed_time(self, end):
         ms = ctypes.c_float()

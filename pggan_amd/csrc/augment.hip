@@ -259,13 +259,13 @@ int pg_augment_u8(int B, int H, int W, const void* src, const float* params, flo
   unsigned char* mid = reinterpret_cast<unsigned char*>(ws);
   unsigned* part = reinterpret_cast<unsigned*>(mid + aug_mid_bytes(B, H, W));
   int* mean = reinterpret_cast<int*>(part + (size_t)B * nblk);
-  hipLaunchKernelGGL(aug_stage1, dim3(nblk, B), dim3(AUG_BLOCK), 0, st,
+  PG_KLAUNCH(aug_stage1, dim3(nblk, B), dim3(AUG_BLOCK), 0, st,
                      reinterpret_cast<const unsigned char*>(src), mid, params, part, H, W);
   PG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(aug_stage2, dim3(B), dim3(AUG_BLOCK), 0, st, part, nblk, mean,
+  PG_KLAUNCH(aug_stage2, dim3(B), dim3(AUG_BLOCK), 0, st, part, nblk, mean,
                      (double)H * (double)W);
   PG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(aug_stage3, dim3(nblk, B), dim3(AUG_BLOCK), 0, st, mid, dst, params, mean, H, W);
+  PG_KLAUNCH(aug_stage3, dim3(nblk, B), dim3(AUG_BLOCK), 0, st, mid, dst, params, mean, H, W);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

@@ -7,6 +7,7 @@
 // tensor layout at the API boundary).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/pggan_hip.h"
@@ -153,6 +154,21 @@ void pg_set_error(const char* fmt, ...);
       pg_set_error(__VA_ARGS__);            \
       return PG_ERR_ARG;                    \
     }                                       \
+  } while (0)
+
+// Every kernel launch of the library goes through PG_KLAUNCH: a launch on the stream an event
+// was armed for (pg_event_arm) records that event at the kernel's completion
+// (hipExtLaunchKernelGGL's stop event, no marker packet of its own in the queue); every other
+// launch is a plain hipLaunchKernelGGL.
+hipEvent_t pg_take_armed_event(hipStream_t s);
+#define PG_KLAUNCH(K, G, B, L, S, ...)                                                     \
+  do {                                                                                    \
+    hipStream_t pgks_ = (S);                                                              \
+    hipEvent_t pgke_ = pg_take_armed_event(pgks_);                                        \
+    if (pgke_)                                                                            \
+      hipExtLaunchKernelGGL(K, G, B, L, pgks_, nullptr, pgke_, 0, __VA_ARGS__);           \
+    else                                                                                  \
+      hipLaunchKernelGGL(K, G, B, L, pgks_, __VA_ARGS__);                                 \
   } while (0)
 
 #define PG_LAUNCH_CHECK()                                                       \

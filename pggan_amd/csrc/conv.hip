@@ -1270,7 +1270,7 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
   static const int red4 = getenv("PG_WG_RED4") ? atoi(getenv("PG_WG_RED4")) : 1;   // A/B switch
   if (red4 && pl.slab >= 65536 && pl.slab % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
     // wide layers (>= 256 blocks of 64 threads): vector form, one thread sums every split
-    hipLaunchKernelGGL(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
+    PG_KLAUNCH(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
                        ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
     PG_LAUNCH_CHECK();
     return PG_OK;
@@ -1280,7 +1280,7 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
   if (ry > pl.splits) ry = pl.splits;
   const int spb = pg_cdiv(pl.splits, ry);
   ry = pg_cdiv(pl.splits, spb);
-  hipLaunchKernelGGL(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, ws, pl.slab, pl.splits, spb,
+  PG_KLAUNCH(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, ws, pl.slab, pl.splits, spb,
                      d->cout * d->cin * 9, dw, db, scale);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1341,7 +1341,7 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   if (need > lds) lds = need;
   PG_CHECK_ARG(lds <= 160 * 1024, "wgrad_bf16: LDS %d too large", lds);
   PG_LDS_ATTR((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), 160 * 1024);
-  hipLaunchKernelGGL((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
+  PG_KLAUNCH((wgrad_bf16_kernel<MO, NC, WMO, WNC, PD, WPE, GZB, BP>), dim3(pl.ot, pl.ct, pl.splits),
                      dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   return wgrad_slab_finish(d, pl, p.mode, ws, dw, db, scale, st);
@@ -1600,7 +1600,7 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
             splits);
   PG_LDS_ATTR((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), 160 * 1024);
-  hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(256), lds, st, p);
+  PG_KLAUNCH((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(256), lds, st, p);
   if (splits > 1) {
     const bool pool = (d->flags & PG_CONV_POOL) != 0;
     const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
@@ -1610,7 +1610,7 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
       PG_CHECK_ARG(d->cout <= 1024 && d->cout % 4 == 0, "conv3x3: split-K PixelNorm needs cout %% 4 == 0, <= 1024");
       blocks = pg_cdiv(d->B * d->H * d->W, 4);
     }
-    hipLaunchKernelGGL(conv_splitk_epilogue<T>, dim3(blocks), dim3(256), 0, st, p, splits);
+    PG_KLAUNCH(conv_splitk_epilogue<T>, dim3(blocks), dim3(256), 0, st, p, splits);
   }
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1748,10 +1748,10 @@ int pg_conv3x3_pack(int dtype, int mode, int cout, int cin, const float* w_oihw,
   const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(pack_kernel<float>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
+    PG_KLAUNCH(pack_kernel<float>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
                        kin, w_oihw, scale, (float*)wpk);
   else
-    hipLaunchKernelGGL(pack_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
+    PG_KLAUNCH(pack_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, mode, cout, cin, rows,
                        kin, w_oihw, scale, (bf16_t*)wpk);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1763,9 +1763,9 @@ int pg_conv3x3_pack_batch(int dtype, int n, const pg_pack_item* items, int max_t
   const dim3 grid(max_tiles, n);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(pack_batch_kernel<float>, grid, dim3(256), 0, st, items);
+    PG_KLAUNCH(pack_batch_kernel<float>, grid, dim3(256), 0, st, items);
   else
-    hipLaunchKernelGGL(pack_batch_kernel<bf16_t>, grid, dim3(256), 0, st, items);
+    PG_KLAUNCH(pack_batch_kernel<bf16_t>, grid, dim3(256), 0, st, items);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1854,9 +1854,9 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(ot, ct, splits);
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(wgrad3x3_kernel<float>, grid, dim3(256), lds, st, p);
+    PG_KLAUNCH(wgrad3x3_kernel<float>, grid, dim3(256), lds, st, p);
   else
-    hipLaunchKernelGGL(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
+    PG_KLAUNCH(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1885,10 +1885,10 @@ int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale,
   }
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(bias_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
+    PG_KLAUNCH(bias_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
                        (const float*)g, scale, db, ppb);
   else
-    hipLaunchKernelGGL(bias_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
+    PG_KLAUNCH(bias_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
                        (const bf16_t*)g, scale, db, ppb);
   PG_LAUNCH_CHECK();
   return PG_OK;

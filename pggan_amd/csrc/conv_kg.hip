@@ -463,7 +463,7 @@ int launch_kg(const pg_conv_desc* d, const void* x, const void* wpk, const float
   p.diag = diag;
   PG_LDS_ATTR((conv_kg_kernel<TH, ONE>), G::LDS);
   const int ntiles = d->B * (d->W / 16) * (d->H / TH);
-  hipLaunchKernelGGL((conv_kg_kernel<TH, ONE>), dim3(ntiles, d->cout / 64), dim3(512), G::LDS, st, p);
+  PG_KLAUNCH((conv_kg_kernel<TH, ONE>), dim3(ntiles, d->cout / 64), dim3(512), G::LDS, st, p);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }

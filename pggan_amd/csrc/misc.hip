@@ -1195,9 +1195,9 @@ __global__ void cast_kernel(size_t n, const A* x, B* y) {
 #define DT_DISPATCH(dtype, KERNEL, grid, block, shm, st, ...)                                  \
   do {                                                                                         \
     if ((dtype) == PG_F32)                                                                     \
-      hipLaunchKernelGGL(KERNEL<float>, grid, block, shm, st, __VA_ARGS__);                    \
+      PG_KLAUNCH(KERNEL<float>, grid, block, shm, st, __VA_ARGS__);                    \
     else if ((dtype) == PG_BF16)                                                               \
-      hipLaunchKernelGGL(KERNEL<bf16_t>, grid, block, shm, st, __VA_ARGS__);                   \
+      PG_KLAUNCH(KERNEL<bf16_t>, grid, block, shm, st, __VA_ARGS__);                   \
     else {                                                                                     \
       pg_set_error("%s: bad dtype %d", __func__, (int)(dtype));                                \
       return PG_ERR_ARG;                                                                       \
@@ -1220,10 +1220,10 @@ int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, v
   const int L = lanes_for(C);
   const size_t threads = (size_t)npix * L;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(pixnorm_fwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0, st,
+    PG_KLAUNCH(pixnorm_fwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0, st,
                        npix, C, cs, L, (const float*)x, (float*)y);
   else
-    hipLaunchKernelGGL(pixnorm_fwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0, st,
+    PG_KLAUNCH(pixnorm_fwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0, st,
                        npix, C, cs, L, (const bf16_t*)x, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1243,11 +1243,11 @@ int pg_pixnorm_lrelu_bwd(int dtype, int npix, int C, int cs, const void* u, cons
   const int L = lanes_for(C);
   const size_t threads = (size_t)npix * L;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(pixnorm_lrelu_bwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0,
+    PG_KLAUNCH(pixnorm_lrelu_bwd_kernel<float>, dim3((threads + 255) / 256), dim3(256), 0,
                        st, npix, C, cs, L, (const float*)u, (const float*)gy, slope, apply_mask,
                        (float*)gz);
   else
-    hipLaunchKernelGGL(pixnorm_lrelu_bwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0,
+    PG_KLAUNCH(pixnorm_lrelu_bwd_kernel<bf16_t>, dim3((threads + 255) / 256), dim3(256), 0,
                        st, npix, C, cs, L, (const bf16_t*)u, (const bf16_t*)gy, slope, apply_mask,
                        (bf16_t*)gz);
   PG_LAUNCH_CHECK();
@@ -1302,11 +1302,11 @@ int pg_unpool_mask(int dtype, int B, int H, int W, int C, int g_cs, const void* 
     return PG_OK;
   }
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(unpool_mask_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+    PG_KLAUNCH(unpool_mask_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        g_cs, (const float*)g, y_cs, (const float*)y, scale, slope, ups, out_cs,
                        (float*)out);
   else
-    hipLaunchKernelGGL(unpool_mask_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+    PG_KLAUNCH(unpool_mask_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        g_cs, (const bf16_t*)g, y_cs, (const bf16_t*)y, scale, slope, ups, out_cs,
                        (bf16_t*)out);
   PG_LAUNCH_CHECK();
@@ -1325,10 +1325,10 @@ int pg_avgpool2(int dtype, int B, int H, int W, int C, int x_cs, const void* x, 
     return PG_OK;
   }
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(avgpool2_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+    PG_KLAUNCH(avgpool2_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        x_cs, (const float*)x, y_cs, (float*)y);
   else
-    hipLaunchKernelGGL(avgpool2_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+    PG_KLAUNCH(avgpool2_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
                        x_cs, (const bf16_t*)x, y_cs, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1345,10 +1345,10 @@ int pg_blend(int dtype, size_t n, float a, const void* x, float b, const void* y
     return PG_OK;
   }
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(blend_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
+    PG_KLAUNCH(blend_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
                        (const float*)x, b, (const float*)y, (float*)out);
   else
-    hipLaunchKernelGGL(blend_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
+    PG_KLAUNCH(blend_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, a,
                        (const bf16_t*)x, b, (const bf16_t*)y, (bf16_t*)out);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1370,10 +1370,10 @@ int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const fl
     return PG_OK;
   }
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(rgb_out_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
+    PG_KLAUNCH(rgb_out_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
                        (const float*)x, w, b, c, Cp, xp_cs, (const float*)xp, wp, bp, cp, alpha, img);
   else
-    hipLaunchKernelGGL(rgb_out_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
+    PG_KLAUNCH(rgb_out_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs,
                        (const bf16_t*)x, w, b, c, Cp, xp_cs, (const bf16_t*)xp, wp, bp, cp, alpha,
                        img);
   PG_LAUNCH_CHECK();
@@ -1394,7 +1394,7 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     dw = nullptr;
   }
   if (gx)
-    hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs, w,
+    PG_KLAUNCH(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, x_cs, w,
                        fa, 0, gimg, gx);
   {
     const size_t npix = (size_t)B * R * R;
@@ -1404,13 +1404,13 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     if (dw) {
       const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       if (C == 16)
-        hipLaunchKernelGGL((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
+        PG_KLAUNCH((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
                            gimg, dw, db);
       else if (C == 32)
-        hipLaunchKernelGGL((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
+        PG_KLAUNCH((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
                            gimg, dw, db);
       else
-        hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
+        PG_KLAUNCH(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
                            0, gimg, dw, db, ppb);
     }
   }
@@ -1423,7 +1423,7 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
       dwp = nullptr;
     }
     if (gxp)
-      hipLaunchKernelGGL(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, Rp, Cp, xp_cs,
+      PG_KLAUNCH(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, Rp, Cp, xp_cs,
                          wp, fp, 1, gimg, gxp);
     const size_t npix = (size_t)B * Rp * Rp;
     int ppb = 1024;
@@ -1432,13 +1432,13 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
     if (dwp) {
       const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       if (Cp == 16)
-        hipLaunchKernelGGL((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
+        PG_KLAUNCH((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
                            1, gimg, dwp, dbp);
       else if (Cp == 32)
-        hipLaunchKernelGGL((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
+        PG_KLAUNCH((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
                            1, gimg, dwp, dbp);
       else
-        hipLaunchKernelGGL(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
+        PG_KLAUNCH(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
                            fp, 1, gimg, dwp, dbp, ppb);
     }
   }
@@ -1489,10 +1489,10 @@ static int from_rgb_impl(int dtype, int B, int R, int C, const ImgSrc& img, int 
     return PG_OK;
   }
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(from_rgb_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
+    PG_KLAUNCH(from_rgb_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
                        down, w, b, c, slope, (const float*)mask_y, y_cs, (float*)y);
   else
-    hipLaunchKernelGGL(from_rgb_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
+    PG_KLAUNCH(from_rgb_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, R, C, img,
                        down, w, b, c, slope, (const bf16_t*)mask_y, y_cs, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1546,10 +1546,10 @@ static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, 
     const int Ri = down ? 2 * R : R;
     const dim3 grid((Ri + 255) / 256, B * Ri);
     if (dtype == PG_F32)
-      hipLaunchKernelGGL(from_rgb_dgrad_kernel<float>, grid, dim3(256), 0, st, R, C, down, w, c,
+      PG_KLAUNCH(from_rgb_dgrad_kernel<float>, grid, dim3(256), 0, st, R, C, down, w, c,
                          gz_cs, (const float*)gz, gimg, ow, norms);
     else
-      hipLaunchKernelGGL(from_rgb_dgrad_kernel<bf16_t>, grid, dim3(256), 0, st, R, C, down, w, c,
+      PG_KLAUNCH(from_rgb_dgrad_kernel<bf16_t>, grid, dim3(256), 0, st, R, C, down, w, c,
                          gz_cs, (const bf16_t*)gz, gimg, ow, norms);
   }
   if (dw || db) {
@@ -1560,23 +1560,23 @@ static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, 
     const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
     if (dtype == PG_F32) {
       if (C == 16)
-        hipLaunchKernelGGL((from_rgb_wgrad_small<float, 16>), dim3(gb), dim3(256), 0, st, B, R, img,
+        PG_KLAUNCH((from_rgb_wgrad_small<float, 16>), dim3(gb), dim3(256), 0, st, B, R, img,
                            down, c, gz_cs, (const float*)gz, dw, db);
       else if (C == 32)
-        hipLaunchKernelGGL((from_rgb_wgrad_small<float, 32>), dim3(gb), dim3(256), 0, st, B, R, img,
+        PG_KLAUNCH((from_rgb_wgrad_small<float, 32>), dim3(gb), dim3(256), 0, st, B, R, img,
                            down, c, gz_cs, (const float*)gz, dw, db);
       else
-        hipLaunchKernelGGL(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C,
+        PG_KLAUNCH(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C,
                            img, down, c, gz_cs, (const float*)gz, dw, db, ppb);
     } else {
       if (C == 16)
-        hipLaunchKernelGGL((from_rgb_wgrad_small<bf16_t, 16>), dim3(gb), dim3(256), 0, st, B, R,
+        PG_KLAUNCH((from_rgb_wgrad_small<bf16_t, 16>), dim3(gb), dim3(256), 0, st, B, R,
                            img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
       else if (C == 32)
-        hipLaunchKernelGGL((from_rgb_wgrad_small<bf16_t, 32>), dim3(gb), dim3(256), 0, st, B, R,
+        PG_KLAUNCH((from_rgb_wgrad_small<bf16_t, 32>), dim3(gb), dim3(256), 0, st, B, R,
                            img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
       else
-        hipLaunchKernelGGL(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
+        PG_KLAUNCH(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
                            img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
     }
   }
@@ -1603,7 +1603,7 @@ int pg_penalty_scale(int mode, int B, float* norms, float w, float* loss_out, fl
                      void* stream) {
   PG_CHECK_ARG(norms && loss_out && scale && B > 0 && (mode == 0 || mode == 1),
                "penalty_scale: bad args");
-  hipLaunchKernelGGL(penalty_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mode, B, norms,
+  PG_KLAUNCH(penalty_scale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, mode, B, norms,
                      w, loss_out, scale);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1613,12 +1613,12 @@ int pg_img_fade(int B, int C, int R, const float* x, float alpha, float* out, vo
   PG_CHECK_ARG(x && out && R % 2 == 0, "img_fade: bad args");
   if (R % 4 == 0 && ((uintptr_t)x & 7) == 0 && ((uintptr_t)out & 7) == 0) {
     const dim3 grid((R / 2 + 255) / 256, B * C * (R / 2));
-    hipLaunchKernelGGL(img_fade_v, grid, dim3(256), 0, (hipStream_t)stream, R, x, alpha, out);
+    PG_KLAUNCH(img_fade_v, grid, dim3(256), 0, (hipStream_t)stream, R, x, alpha, out);
     PG_LAUNCH_CHECK();
     return PG_OK;
   }
   const size_t n = (size_t)B * C * R * R;
-  hipLaunchKernelGGL(img_fade_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, B, C, R,
+  PG_KLAUNCH(img_fade_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, B, C, R,
                      x, alpha, out);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1697,7 +1697,7 @@ int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const voi
   const size_t n = (size_t)d->N * d->K;
   hipStream_t st = (hipStream_t)stream;
   if (lin_fast_ok(dtype, d) && ((uintptr_t)dw & 15) == 0) {   // bf16: coalesced dw streaming
-    hipLaunchKernelGGL(lin_wgrad_v<bf16_t>, dim3((d->K + 1023) / 1024, d->N), dim3(256), 0, st, *d, x,
+    PG_KLAUNCH(lin_wgrad_v<bf16_t>, dim3((d->K + 1023) / 1024, d->N), dim3(256), 0, st, *d, x,
                        gy, dw, db);
     PG_LAUNCH_CHECK();
     return PG_OK;
@@ -1713,10 +1713,10 @@ int pg_mbstd_fwd(int dtype, int B, int HW, int C, int x_cs, const void* x, int y
   const int G = mbstd_group(B);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
-    hipLaunchKernelGGL(mbstd_fwd_kernel<float>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
+    PG_KLAUNCH(mbstd_fwd_kernel<float>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
                        (const float*)x, y_cs, (float*)y);
   else
-    hipLaunchKernelGGL(mbstd_fwd_kernel<bf16_t>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
+    PG_KLAUNCH(mbstd_fwd_kernel<bf16_t>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
                        (const bf16_t*)x, y_cs, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1729,14 +1729,14 @@ template <typename T>
 static void mbstd_bwd_launch(int B, int HW, int C, int x_cs, const void* x, int y_cs, const void* gy,
                              void* gx, hipStream_t st) {
   const int G = mbstd_group(B);
-  hipLaunchKernelGGL(mbstd_bwd_kernel<T>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
+  PG_KLAUNCH(mbstd_bwd_kernel<T>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs,
                      (const T*)x, y_cs, (const T*)gy, (T*)gx);
 }
 template <typename T>
 static void mbstd_r1_launch(int B, int HW, int C, int x_cs, const void* x, const void* a, int y_cs,
                             const void* gy, void* tout, void* inj, hipStream_t st) {
   const int G = mbstd_group(B);
-  hipLaunchKernelGGL(mbstd_r1_kernel<T>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs, (const T*)x,
+  PG_KLAUNCH(mbstd_r1_kernel<T>, dim3(B / G, PG_MBSTD_SLICES), dim3(1024), 0, st, B, HW, C, x_cs, (const T*)x,
                      (const T*)a, y_cs, (const T*)gy, (T*)tout, (T*)inj);
 }
 
@@ -1765,7 +1765,7 @@ int pg_mbstd_r1(int dtype, int B, int HW, int C, int x_cs, const void* x, const 
 int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out, float* u,
                 float* h, void* stream) {
   PG_CHECK_ARG(logits && B > 0, "bce_loss: bad args");
-  hipLaunchKernelGGL(bce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, target, w,
+  PG_KLAUNCH(bce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, target, w,
                      loss_out, u, h);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1773,7 +1773,7 @@ int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out
 
 int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u, void* stream) {
   PG_CHECK_ARG(logits && B > 0, "drift_loss: bad args");
-  hipLaunchKernelGGL(drift_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, w,
+  PG_KLAUNCH(drift_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, B, logits, w,
                      loss_out, u);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1781,7 +1781,7 @@ int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u
 
 int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream) {
   PG_CHECK_ARG(g && r1_out && B > 0, "r1_penalty: bad args");
-  hipLaunchKernelGGL(r1_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, (hipStream_t)stream, B,
+  PG_KLAUNCH(r1_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, (hipStream_t)stream, B,
                      n, g, r1_out, gbar);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1790,7 +1790,7 @@ int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, v
 int pg_gp_interp(int B, size_t per, const float* xr, const float* xf, const float* eps,
                  float* out, void* stream) {
   PG_CHECK_ARG(xr && xf && eps && out, "gp_interp: bad args");
-  hipLaunchKernelGGL(gp_interp_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0,
+  PG_KLAUNCH(gp_interp_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0,
                      (hipStream_t)stream, B, per, xr, xf, eps, out);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1802,8 +1802,8 @@ int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, flo
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(norms, 0, sizeof(float) * B, st);
   int gx = grid_for(per, 256, 256);
-  hipLaunchKernelGGL(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms);
-  hipLaunchKernelGGL(gp_finish_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0, st, B, per, g,
+  PG_KLAUNCH(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms);
+  PG_KLAUNCH(gp_finish_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0, st, B, per, g,
                      w, norms, gp_out, gbar);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1812,7 +1812,7 @@ int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, flo
 int pg_mul_add(size_t n, const float* x, const float* y, const float* z, float* out,
                void* stream) {
   PG_CHECK_ARG(x && y && z && out, "mul_add: null pointer");
-  hipLaunchKernelGGL(mul_add_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, y,
+  PG_KLAUNCH(mul_add_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, y,
                      z, out);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1825,7 +1825,7 @@ int pg_adam(size_t n, float* p, const float* g, float* m, float* v, float lr, fl
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
   const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
+  PG_KLAUNCH(adam_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m,
                      v, beta1, beta2, eps, step_size, bc2_sqrt);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1855,8 +1855,8 @@ int pg_adam_dev(size_t n, float* p, const float* g, float* m, float* v, float be
                 float eps, const float* table, int tlen, int* step, void* stream) {
   PG_CHECK_ARG(p && g && m && v && table && step && tlen >= 1, "adam_dev: bad args");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(counter_tick_kernel, dim3(1), dim3(1), 0, st, step);
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, p, g, m, v, beta1,
+  PG_KLAUNCH(counter_tick_kernel, dim3(1), dim3(1), 0, st, step);
+  PG_KLAUNCH(adam_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, p, g, m, v, beta1,
                      beta2, eps, table, tlen, (const int*)step);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1868,6 +1868,27 @@ static int pg_hip_status(hipError_t e, const char* what) {
   pg_set_error("%s: %s", what, hipGetErrorString(e));
   return PG_ERR_HIP;
 }
+
+}  // extern "C"
+// the event armed for the next launch on one stream (per host thread)
+static thread_local hipEvent_t g_arm_ev = nullptr;
+static thread_local hipStream_t g_arm_st = nullptr;
+
+hipEvent_t pg_take_armed_event(hipStream_t s) {
+  if (!g_arm_ev || s != g_arm_st) return nullptr;
+  hipEvent_t e = g_arm_ev;
+  g_arm_ev = nullptr;
+  return e;
+}
+extern "C" {
+
+int pg_event_arm(void* ev, void* stream) {
+  g_arm_ev = (hipEvent_t)ev;
+  g_arm_st = (hipStream_t)stream;
+  return PG_OK;
+}
+
+int pg_event_armed(void) { return g_arm_ev != nullptr; }
 
 int pg_event_create(int timing, void** ev) {
   PG_CHECK_ARG(ev, "event_create: null out");
@@ -1912,16 +1933,16 @@ int pg_event_destroy(void* ev) {
 int pg_randn_dev(size_t n, uint64_t seed, uint64_t* offset, float* out, void* stream) {
   PG_CHECK_ARG(out && offset, "randn_dev: null pointer");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(randn_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, seed,
+  PG_KLAUNCH(randn_dev_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, seed,
                      (const uint64_t*)offset, out);
-  hipLaunchKernelGGL(u64_add_kernel, dim3(1), dim3(1), 0, st, offset, (uint64_t)n);
+  PG_KLAUNCH(u64_add_kernel, dim3(1), dim3(1), 0, st, offset, (uint64_t)n);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
 
 int pg_randn(size_t n, uint64_t seed, uint64_t offset, float* out, void* stream) {
   PG_CHECK_ARG(out, "randn: null out");
-  hipLaunchKernelGGL(randn_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, seed,
+  PG_KLAUNCH(randn_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, seed,
                      offset, out);
   PG_LAUNCH_CHECK();
   return PG_OK;
@@ -1931,16 +1952,16 @@ int pg_cast(int dtype_in, int dtype_out, size_t n, const void* x, void* y, void*
   PG_CHECK_ARG(x && y, "cast: null pointer");
   hipStream_t st = (hipStream_t)stream;
   if (dtype_in == PG_F32 && dtype_out == PG_BF16)
-    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
+    PG_KLAUNCH((cast_kernel<float, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
                        (const float*)x, (bf16_t*)y);
   else if (dtype_in == PG_BF16 && dtype_out == PG_F32)
-    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
+    PG_KLAUNCH((cast_kernel<bf16_t, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
                        (const bf16_t*)x, (float*)y);
   else if (dtype_in == PG_F32 && dtype_out == PG_F32)
-    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
+    PG_KLAUNCH((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, n,
                        (const float*)x, (float*)y);
   else
-    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
+    PG_KLAUNCH((cast_kernel<bf16_t, bf16_t>), dim3(grid_for(n)), dim3(256), 0, st, n,
                        (const bf16_t*)x, (bf16_t*)y);
   PG_LAUNCH_CHECK();
   return PG_OK;

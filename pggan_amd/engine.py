@@ -224,6 +224,7 @@ class StepEngine:
         self.side = None
         self._side_ev = {}      # buffer-set key -> last side-stream event reading it
         self._side_pending = []  # queued side launches (side_batch > 1, see _side_call)
+        self._armed_ev = None    # the event the next main-stream launch records (armed form)
         self.side_batch = max(1, int(os.environ.get("PG_SIDE_BATCH", "1")))
         self.ws_side = None
         self._dkey = "D"        # key of the D buffer set in use ("Df": the fake-image pass)
@@ -261,6 +262,10 @@ class StepEngine:
         if (self.side is not None and hasattr(ops, "event") and
                 os.environ.get("PG_TORCH_EVENTS", "0") != "1"):
             self._ev_ring = [ops.event() for _ in range(512)]
+        # PG_ARM_EVENTS=1: the side stream's waits on the main stream use events recorded by
+        # the main kernels themselves (see _side_call)
+        self._arm_events = (self._ev_ring is not None and
+                            os.environ.get("PG_ARM_EVENTS", "0") == "1")
         self._alloc()
 
     def _event(self):
@@ -510,6 +515,16 @@ class StepEngine:
         before the side workspace is replaced."""
         if self.side is None or FORCE_SERIAL:
             return fn(*a, **kw)
+        if self._arm_events and not torch.cuda.is_current_stream_capturing():
+            # armed form: this launch waits for an event the NEXT main-stream kernel of the
+            # library records at its completion (pg_event_arm: no marker packet in the main
+            # queue); it is enqueued at the next side call or flush, one main kernel later
+            self._side_flush()
+            self._side_pending.append((nets, fn, a, kw))
+            ev = self._event()
+            ev.arm(torch.cuda.current_stream())
+            self._armed_ev = ev
+            return
         self._side_pending.append((nets, fn, a, kw))
         if len(self._side_pending) >= self.side_batch:
             self._side_flush()
@@ -518,7 +533,14 @@ class StepEngine:
         if not self._side_pending:
             return
         pend, self._side_pending = self._side_pending, []
-        self._side_wait_main()
+        ev, self._armed_ev = self._armed_ev, None
+        if ev is not None:
+            if self.ops.lib.pg_event_armed():   # no library launch on the main stream since
+                self.ops.lib.pg_event_arm(None, None)
+                ev.record(torch.cuda.current_stream())
+            ev.wait(self.side)
+        else:
+            self._side_wait_main()
         with torch.cuda.stream(self.side):
             for _, fn, a, kw in pend:
                 fn(*a, **kw)
