@@ -1206,7 +1206,8 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // cin > 32; below 32^2 the single-half tile is faster
   // PG_WG_DMA16=1: the 16^2 wide layers on wgrad_dma_kernel too (it needs WNC = 2); measured
   // 28.6 vs 24.1 us for the register-staged single-half tile at 16^2 512 -> 512, so off
-  static const int dma16 = getenv("PG_WG_DMA16") ? atoi(getenv("PG_WG_DMA16")) : 0;
+  const char* dma16_env = getenv("PG_WG_DMA16");   // per call: the op tests switch it
+  const int dma16 = dma16_env ? atoi(dma16_env) : 0;
   const bool w16_dma = dma16 && d->W == 16 && d->H % 8 == 0 && co % 64 == 0 && ci % 32 == 0 &&
                        !(d->flags & PG_CONV_GZ_BITS);
   pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32 || w16_dma) ? 2 : 1;

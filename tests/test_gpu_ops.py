@@ -77,7 +77,7 @@ CONV_CASES = [
     (8, 128, 64, 64, ("ups", "bias", "lrelu", "pool")),
     (4, 128, 128, 128, ("mask", "accum")),
     # tile 3 with more tiles than one round of workgroups (the default one-tile-per-workgroup
-    # launch; the opt-in persistent form, PG_HR_MT=1, is not run by this suite): one chunk
+    # launch; the opt-in persistent form, PG_HR_MT=1: test_conv3x3_fwd_opt_in): one chunk
     # with the pre-pool copy, two chunks x two output-channel blocks, two chunks with bias
     (4, 256, 32, 64, ("bias", "lrelu", "pool")),
     (2, 256, 64, 128, ("mask", "accum")),
@@ -152,7 +152,7 @@ WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, Fa
                (4, 128, 16, 32, False), (4, 32, 512, 512, False), (2, 64, 32, 16, True),
                (4, 64, 64, 128, False),
                # the 16^2 wide layer (the register-staged kernel by default; the opt-in LDS-DMA
-               # form, PG_WG_DMA16=1, is not run by this suite) and the LDS-DMA kernel with ups
+               # form, PG_WG_DMA16=1: test_conv3x3_wgrad_dma16_opt_in) and the LDS-DMA kernel with ups
                (4, 16, 512, 512, False), (2, 64, 256, 128, True)]
 
 
@@ -490,6 +490,25 @@ def test_conv_kg(case, monkeypatch):
     cmp(outs[0][0], outs[1][0], 2e-2, "kg y")
     if outs[0][1] is not None:
         cmp(outs[0][1], outs[1][1], 2e-2, "kg y2")
+
+
+@pytest.mark.parametrize("knob,case", [
+    # the opt-in persistent multi-tile form of tile 3 (PG_HR_MT=1): more tiles than one round
+    ("PG_HR_MT", (4, 256, 32, 64, ("bias", "lrelu", "pool"))),
+    ("PG_HR_MT", (2, 256, 64, 128, ("mask", "accum"))),
+    ("PG_HR_MT", (4, 256, 64, 64, ("bias", "lrelu"))),
+])
+def test_conv3x3_fwd_opt_in(knob, case, monkeypatch):
+    """The off-by-default kernels that ship in the library, switched on per call."""
+    monkeypatch.setenv(knob, "1")
+    test_conv3x3_fwd(case, torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", [(4, 16, 512, 512, False)])
+def test_conv3x3_wgrad_dma16_opt_in(case, monkeypatch):
+    """The LDS-DMA weight gradient at 16^2 (PG_WG_DMA16=1, off by default)."""
+    monkeypatch.setenv("PG_WG_DMA16", "1")
+    test_conv3x3_wgrad(case, torch.bfloat16, True)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
