@@ -61,6 +61,9 @@ class GradExchange:
         self._state = {}
         self.calls = 0          # collectives launched, and the host seconds spent in them
         self.host_s = 0.0
+        # set by the engine around ready(): called once before ready() launches a collective
+        # (the side stream's wait for the main stream, needed only then)
+        self.before_launch = None
 
     def bind(self, net, fp):
         """fp: the net's engine.FlatParams (live parameters first)."""
@@ -105,6 +108,8 @@ class GradExchange:
             st["pend"].append((lo, hi))
             st["pend_elems"] += hi - lo
         if st["pend_elems"] * 4 >= self.bucket_bytes:
+            if self.before_launch is not None:
+                self.before_launch()
             self._launch_merged(net, st["pend"])
             st["pend"], st["pend_elems"] = [], 0
 
