@@ -368,6 +368,10 @@ int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);
  * stream's next kernel by ~6.5 us on MI355X.  pg_event_armed() is 1 while the event still waits
  * for its launch (then record it with pg_event_record). */
 int pg_event_arm(void* ev, void* stream);
+/* A non-blocking stream of the library's own; lowest_priority != 0: at the device's least
+ * priority (its own hardware-queue pool, so never the queue of a normal-priority stream) */
+int pg_stream_create(int lowest_priority, void** stream);
+int pg_stream_destroy(void* stream);
 int pg_event_armed(void);
 int pg_event_destroy(void* ev);
 

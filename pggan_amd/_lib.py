@@ -161,6 +161,8 @@ _SIGS = {
     "pg_event_elapsed_ms": ([_VP, _VP, ctypes.POINTER(ctypes.c_float)], _I),
     "pg_event_destroy": ([_VP], _I),
     "pg_event_arm": ([_VP, _VP], _I),
+    "pg_stream_create": ([_I, ctypes.POINTER(ctypes.c_void_p)], _I),
+    "pg_stream_destroy": ([_VP], _I),
     "pg_event_armed": ([], _I),
 }
 SYMBOLS = ["pg_last_error"] + list(_SIGS)
@@ -263,6 +265,13 @@ class HipOps:
         return PG_F32 if t.dtype == torch.float32 else PG_BF16
 
     # -- stream ordering -----------------------------------------------------
+    def stream(self, lowest_priority=False):
+        """A torch.cuda.ExternalStream over pg_stream_create (lives as long as the process)."""
+        h = ctypes.c_void_p()
+        self._chk(self.lib.pg_stream_create(int(bool(lowest_priority)), ctypes.byref(h)),
+                  "stream_create")
+        return torch.cuda.ExternalStream(h.value)
+
     def event(self, timing=False):
         """A HipEvent (device-scope release; see pg_event_create)."""
         return HipEvent(self, timing)

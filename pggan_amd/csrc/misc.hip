@@ -1882,6 +1882,24 @@ hipEvent_t pg_take_armed_event(hipStream_t s) {
 }
 extern "C" {
 
+int pg_stream_create(int lowest_priority, void** stream) {
+  PG_CHECK_ARG(stream, "stream_create: null out");
+  int least = 0, greatest = 0;
+  int rc = pg_hip_status(hipDeviceGetStreamPriorityRange(&least, &greatest),
+                         "hipDeviceGetStreamPriorityRange");
+  if (rc != PG_OK) return rc;
+  hipStream_t s = nullptr;
+  rc = pg_hip_status(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, lowest_priority ? least : 0),
+                     "hipStreamCreateWithPriority");
+  *stream = rc == PG_OK ? (void*)s : nullptr;
+  return rc;
+}
+
+int pg_stream_destroy(void* stream) {
+  if (!stream) return PG_OK;
+  return pg_hip_status(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
+}
+
 int pg_event_arm(void* ev, void* stream) {
   g_arm_ev = (hipEvent_t)ev;
   g_arm_st = (hipStream_t)stream;

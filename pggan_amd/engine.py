@@ -230,7 +230,16 @@ class StepEngine:
         self._dkey = "D"        # key of the D buffer set in use ("Df": the fake-image pass)
         if (forward_only is None and str(device).startswith("cuda") and
                 os.environ.get("PG_SIDE_WGRAD", "1") != "0"):
-            self.side = torch.cuda.Stream(device=device)
+            # the side stream at the device's least priority, created by the library: its own
+            # hardware-queue pool, so it never shares the main stream's queue.  With 16 queues
+            # per process (DP runs) a torch pool stream landed on the main stream's queue and
+            # serialised the two (DP bookkeeping at one rank: 301 vs 351 img/s; with this
+            # stream 339.5; without DP 351.0 vs 350.3, profiles/r4_side_queue_ab.txt).
+            # PG_SIDE_LOWPRI=0: a torch pool stream (A/B runs).
+            if os.environ.get("PG_SIDE_LOWPRI", "1") != "0" and hasattr(ops, "stream"):
+                self.side = ops.stream(lowest_priority=True)
+            else:
+                self.side = torch.cuda.Stream(device=device)
         # the fake-image pass of the D half (G forward, D forward + backward) depends on the
         # real-image part (F, B1, R1, T, B2) only through the parameters, so it runs on its
         # own stream beside it, with its own D buffer set, split-K workspace, weight-gradient
