@@ -80,9 +80,6 @@ int pg_version(void);
  * gradient through an upsampling conv a, then the previous block's PixelNorm).  Not with
  * BIAS / MASK / ACCUM / PIXNORM / bit flags. */
 #define PG_CONV_PNBWD 2048
-/* Channel-blocked activations: the operand is [B][C/32][H][W][32] (C = its channel stride,
- * a multiple of 32) instead of NHWC -- a 32-channel slice of a pixel row is contiguous. */
-#define PG_CONV_X_BLK 4096
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
