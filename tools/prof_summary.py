@@ -140,6 +140,34 @@ def gap_stats(path):
                 avg_gap_us=gaps / 1e3 / max(small, 1))
 
 
+def steady_state(path, steps=3):
+    """Launches and kernel time per step over the last `steps` steps of the trace (delimited
+    by the adam_dev_kernel launches, two per step): the whole-trace stats include the setup
+    (buffer allocation fills, copies) and the warm-up, which a per-step count must not."""
+    path = _resolve(path, "kernel_trace.csv")
+    ev = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"],
+                       short(r["Kernel_Name"]).split("<")[0]))
+    ev.sort()
+    ad = [i for i, e in enumerate(ev) if e[3] == "adam_dev_kernel"]
+    if len(ad) < 2 * steps + 1:
+        return None
+    w = ev[ad[-1 - 2 * steps] + 1:ad[-1] + 1]
+    per = defaultdict(lambda: [0, 0.0])
+    queues = defaultdict(int)
+    for s, e, q, n in w:
+        per[n][0] += 1
+        per[n][1] += (e - s) / 1e3
+        queues[q] += 1
+    return dict(steps=steps, ms_per_step=(w[-1][1] - w[0][0]) / 1e6 / steps,
+                launches_per_step=len(w) / steps,
+                launches_per_step_by_queue={q: c / steps for q, c in sorted(queues.items())},
+                kernels={n: dict(per_step=c / steps, us_per_step=round(t / steps, 1))
+                         for n, (c, t) in sorted(per.items(), key=lambda kv: -kv[1][0])})
+
+
 def read_trace(path):
     path = _resolve(path, "kernel_trace.csv")
     fam = defaultdict(lambda: dict(ns=0, calls=0, dispatches=0))
@@ -201,7 +229,7 @@ def main():
     a = ap.parse_args()
     fam, per_kernel, total = read_trace(a.trace)
     res = {"config": a.config, "total_kernel_ms": total / 1e6, "families": {},
-           "top_kernels": [], "gaps": gap_stats(a.trace)}
+           "top_kernels": [], "gaps": gap_stats(a.trace), "steady_state": steady_state(a.trace)}
     for k, v in fam.items():
         res["families"][k] = dict(total_ms=v["ns"] / 1e6, calls=v["calls"],
                                   dispatches=v["dispatches"],
