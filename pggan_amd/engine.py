@@ -25,6 +25,7 @@ images NCHW fp32, parameters/gradients/Adam state fp32 in flat buffers.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass
@@ -323,7 +324,23 @@ class StepEngine:
             g["gh0"] = t(B, 4, 4, d[0])
             g["gzf"] = t(B, 4, 4, d[0])
         # ---- D
-        self.dd = self._alloc_D(need_D, train)
+        # the D half's real and fake passes share one forward and one second backward at
+        # batch 2B (see _merged): the D buffers are allocated at 2B ([real; fake] along the
+        # batch), self.dd holds first-half views (every batch-B pass: B1, the tangent, the G
+        # half) and the generator's image is the second half of the merged input.  Needs
+        # B % 4 == 0 so the minibatch-stddev groups (4 contiguous samples) stay within a half.
+        # PG_MERGE_D=0: separate passes (A/B runs).
+        self.dd2 = None
+        self._Bs = (B,)
+        if (fo is None and B % 4 == 0 and os.environ.get("PG_MERGE_D", "1") != "0"):
+            self._Bs = (B, 2 * B)
+            self.dd2 = self._alloc_D(need_D, train, 2 * B)
+            self.dd2["xin"] = t(2 * B, 3, R, R, f32=True)
+            self.dd = {k: v[:B] for k, v in self.dd2.items()}
+            self.dd_hi = {k: v[B:] for k, v in self.dd2.items()}
+            g["img"] = self.dd2["xin"][B:]
+        else:
+            self.dd = self._alloc_D(need_D, train)
         # the fake-image pass's buffer set (concurrent mode) and its split-K workspace
         self.dd_f = self._alloc_D(need_D, train) if self.fstream is not None else None
         self.ws_f = torch.empty_like(self.ws) if (self.fstream is not None and self.ws is not None) \
@@ -331,8 +348,9 @@ class StepEngine:
         # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
         self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
 
-    def _alloc_D(self, need_D, train):
-        B, s, d, R = self.B, self.s, self.depths, self.R
+    def _alloc_D(self, need_D, train, B=None):
+        B = self.B if B is None else B
+        s, d, R = self.s, self.depths, self.R
         t = self._t
         D = {}
         if need_D:
@@ -474,7 +492,7 @@ class StepEngine:
 
     def _ws_bytes(self, kind, H, cin, cout, ups):
         """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape)."""
-        key = (kind, H, cin, cout, ups)
+        key = (kind, H, cin, cout, ups, self.B)
         need = self._ws_cache.get(key)
         if need is None:
             if kind == "c":
@@ -588,6 +606,15 @@ class StepEngine:
                 else:
                     ev.wait(cur)
 
+    def _conv_sup(self):
+        """ops.conv_supported at every batch size the D passes run (B, and 2B when the D
+        half's passes are merged): a sign-bit layout decided once serves both."""
+        f = getattr(self.ops, "conv_supported", None)
+        if f is None:
+            return None
+        Bs = self._Bs
+        return lambda B, **kw: all(f(B=b, **kw) for b in Bs)
+
     def _dbits(self, i):
         """Whether D level i keeps its conv-b (conv + lrelu + pool) output as sign bits only:
         the forward writes bits instead of the full-resolution activation, and every consumer
@@ -595,7 +622,7 @@ class StepEngine:
         and the pooled-resolution gradient directly (no unpool_mask pass)."""
         key = ("dbits", i, 0, 0, 0)
         if key not in self._ws_cache:
-            f = getattr(self.ops, "conv_supported", None)
+            f = self._conv_sup()
             d, Ri = self.depths, 8 * 2 ** i
             # below 512^2 the saved bytes no longer pay for the masking work in the staging
             ok = bool(self.fuse_dbits and f is not None and d[i] % 16 == 0 and
@@ -621,7 +648,7 @@ class StepEngine:
         input-gradient conv and the weight gradient.  PG_UBITS=0: off (A/B runs)."""
         key = ("ubits", i, 0, 0, 0)
         if key not in self._ws_cache:
-            f = getattr(self.ops, "conv_supported", None)
+            f = self._conv_sup()
             d, Ri, B = self.depths, 8 * 2 ** i, self.B
             ok = bool(f is not None and self.fuse_dbits and not self._dbits(i) and
                       os.environ.get("PG_UBITS", "1") != "0" and d[i] % 16 == 0)
@@ -645,7 +672,7 @@ class StepEngine:
         (profiles/r4_bits_ab.txt)."""
         key = ("abits", i, 0, 0, 0)
         if key not in self._ws_cache:
-            f = getattr(self.ops, "conv_supported", None)
+            f = self._conv_sup()
             d, Ri, B = self.depths, 8 * 2 ** i, self.B
             ok = bool(self._dbits(i) and os.environ.get("PG_ABITS", "0") == "1" and
                       d[i + 1] % 16 == 0)
@@ -666,7 +693,7 @@ class StepEngine:
         PG_RGBBITS=0: off (A/B runs)."""
         key = ("rgbbits", 0, 0, 0, 0)
         if key not in self._ws_cache:
-            f = getattr(self.ops, "conv_supported", None)
+            f = self._conv_sup()
             d, s, R, B = self.depths, self.s, self.R, self.B
             ok = bool(f is not None and self.fuse_dbits and s >= 1 and
                       os.environ.get("PG_RGBBITS", "1") != "0" and d[s] % 8 == 0 and
@@ -1181,6 +1208,8 @@ class StepEngine:
         GD_flat.zero_()
         self.loss[:3].zero_()
         self.loss[4:5].zero_()
+        if self._merged():
+            return self._d_step_merged(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake)
         conc = self.fstream is not None and hp.gp_mode == "r1"
         if conc:
             ev0 = torch.cuda.Event()   # the fake pass starts from here, beside the real part
@@ -1220,6 +1249,79 @@ class StepEngine:
             self._wgan_gp(PD, GD, xr, img_fake, gp_eps, alpha_D)
         self._side_join()
         return xr, img_fake
+
+    def _merged(self):
+        """Whether this D half runs its real and fake passes merged (batch 2B): the R1 mode,
+        2B buffers allocated, no concurrent fake stream, and no generator update still
+        waiting for its DP exchange (that exchange overlaps the real-image part of the
+        separate schedule, which does not read G; the merged forward needs the fake image
+        first)."""
+        return (self.dd2 is not None and self.hyper.gp_mode == "r1" and self.fstream is None and
+                not hasattr(self._pending_G, "wait"))
+
+    @contextlib.contextmanager
+    def _pair(self):
+        """Run the enclosed passes at batch 2B on the merged buffers."""
+        saved = (self.dd, self.B)
+        self.dd, self.B = self.dd2, 2 * saved[1]
+        try:
+            yield
+        finally:
+            self.dd, self.B = saved
+
+    def _d_step_merged(self, PG, PD, GD, real, z, alpha_G, alpha_D, before_fake):
+        """The R1 D half with the fake image's passes merged into the real image's
+        (pggan/model.py:211-238; the same terms, batch [real; fake] = 2B):
+          G forward (the fake image straight into the second half of the merged input),
+          F over both images, the two BCE terms (each over its own half, so each is the
+          reference's mean over B), B1 + R1 + T on the real half at batch B, then ONE
+          second backward over both halves -- upstream u2 = u + tout * hl for the real
+          samples and the fake BCE gradient for the fake ones -- whose weight gradients are
+          the sum of the two passes'.  Every per-sample quantity is the separate schedule's
+          (convs and mbstd groups never mix samples of the two halves); only the order in
+          which the weight gradients sum over samples differs.  Half the D forward and
+          second-backward launches, at twice the work each: the 4^2-32^2 levels are latency
+          bound and the wide levels amortise each launch's ramp and epilogue."""
+        ops, hp = self.ops, self.hyper
+        B = self.B
+        D1, D2 = self.dd, self.dd2
+        X = D2["xin"]
+        if before_fake is not None:
+            before_fake()
+        img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
+        if self._low(alpha_D):
+            ops.img_fade(real, alpha_D, X[:B])                                   # :217-221
+        else:
+            X[:B].copy_(real)
+        trace, self.trace = self.trace, None
+        try:
+            with self._pair():
+                self.d_forward(PD, X, alpha_D)                                  # :216, :228
+        finally:
+            self.trace = trace
+        h2 = self.h_mb
+        self.h_mb = h2[:B]
+        if trace is not None:   # one record per image, in the separate schedule's order
+            trace("D", self)
+            self.dd = self.dd_hi
+            try:
+                trace("D", self)
+            finally:
+                self.dd = D1
+        ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], D1["hl"])    # lib/loss.py:119-123
+        ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u2"][B:], None)
+        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1")                     # lib/loss.py:125-135
+        tout, inj = self.d_tangent(PD, GD, gbar, D1["u"], alpha_D)
+        ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
+        self.h_mb = h2
+        try:
+            with self._pair():
+                # D2["inj"]: the tangent wrote the real half; the fake half stays zero
+                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True)
+        finally:
+            self.h_mb = h2[:B]
+        self._side_join()
+        return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
 
     def _fake_pass_concurrent(self, PG, PD, z, alpha_G, alpha_D, ev0, before_fake):
         """The fake-image part of the D half on self.fstream with the second buffer set
