@@ -297,8 +297,20 @@ class StepEngine:
         # "Dtrain" (that net's forward + first-order backward: the autograd modules)
         need_G, need_D = fo in (None, "G", "Gtrain"), fo in (None, "D", "Dtrain")
         train = fo in (None, "Gtrain", "Dtrain")
+        merge_d = fo is None and B % 4 == 0 and os.environ.get("PG_MERGE_D", "1") != "0"
+        # the D half's generator forward (the fake image) and the G half's use the same G
+        # parameters (Adam_G runs after the G half): with merge_g they run as ONE forward at
+        # batch 2B ([fake for D; fake for G], see _d_step_merged); the G buffers are
+        # allocated at 2B, self.g holds first-half views and g_hi the G half's.
+        # PG_MERGE_G=0: separate forwards (A/B runs).
+        merge_g = merge_d and os.environ.get("PG_MERGE_G", "1") != "0"
+        GB = 2 * B if merge_g else B
+        self._GBs = (B, 2 * B) if merge_g else (B,)
+        self._g_done = False
+        self._z_g = None
         # ---- G
         self.g = g = {}
+        B0, B = B, GB
         if need_G:
             g["z"] = t(B, self.latent, f32=True)
             g["zn"] = t(B, self.latent, f32=True)
@@ -323,6 +335,13 @@ class StepEngine:
             g["gz0"] = t(B, 4, 4, d[0])
             g["gh0"] = t(B, 4, 4, d[0])
             g["gzf"] = t(B, 4, 4, d[0])
+        B = B0
+        self.g2 = self.g_hi = None
+        if merge_g and need_G:
+            self.g2 = g
+            self.g = g = {k: v[:B] for k, v in self.g2.items()}
+            self.g_hi = {k: v[B:] for k, v in self.g2.items()}
+        self.g_lo = g
         # ---- D
         # the D half's real and fake passes share one forward and one second backward at
         # batch 2B (see _merged): the D buffers are allocated at 2B ([real; fake] along the
@@ -332,13 +351,19 @@ class StepEngine:
         # PG_MERGE_D=0: separate passes (A/B runs).
         self.dd2 = None
         self._Bs = (B,)
-        if (fo is None and B % 4 == 0 and os.environ.get("PG_MERGE_D", "1") != "0"):
+        if merge_d:
             self._Bs = (B, 2 * B)
             self.dd2 = self._alloc_D(need_D, train, 2 * B)
-            self.dd2["xin"] = t(2 * B, 3, R, R, f32=True)
+            # the images [real; fake for D; fake for G]: D's merged input is the first two
+            # thirds, the generator writes the last two
+            x3 = t(3 * B, 3, R, R, f32=True)
+            self.dd2["xin"] = x3[:2 * B]
             self.dd = {k: v[:B] for k, v in self.dd2.items()}
             self.dd_hi = {k: v[B:] for k, v in self.dd2.items()}
-            g["img"] = self.dd2["xin"][B:]
+            g["img"] = x3[B:2 * B]
+            if self.g2 is not None:
+                self.g2["img"] = x3[B:]
+                self.g_hi["img"] = x3[2 * B:]
         else:
             self.dd = self._alloc_D(need_D, train)
         # the fake-image pass's buffer set (concurrent mode) and its split-K workspace
@@ -490,23 +515,24 @@ class StepEngine:
                          bias=bs if (flags & L.CONV_BIAS) else None, aux=aux, y2=y2,
                          ws=self.ws if need else None, **kw)
 
-    def _ws_bytes(self, kind, H, cin, cout, ups):
+    def _ws_bytes(self, kind, H, cin, cout, ups, B=None):
         """Split-reduction workspace bytes of a conv / wgrad launch (cached per shape)."""
-        key = (kind, H, cin, cout, ups, self.B)
+        B = self.B if B is None else B
+        key = (kind, H, cin, cout, ups, B)
         need = self._ws_cache.get(key)
         if need is None:
             if kind == "c":
-                need = self.ops.conv_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout)
+                need = self.ops.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
             else:
-                need = self.ops.wgrad_workspace_bytes(B=self.B, H=H, W=H, cin=cin, cout=cout,
+                need = self.ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout,
                                                       ups=ups)
             self._ws_cache[key] = need
         return need
 
-    def _ws_need(self, kind, H, cin, cout, ups):
+    def _ws_need(self, kind, H, cin, cout, ups, B=None):
         """_ws_bytes, growing the main stream's shared workspace to the largest need
         (launches on one stream are ordered)."""
-        need = self._ws_bytes(kind, H, cin, cout, ups)
+        need = self._ws_bytes(kind, H, cin, cout, ups, B)
         if need and (self.ws is None or self.ws.numel() * 4 < need):
             self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         return need
@@ -724,11 +750,12 @@ class StepEngine:
         key = ("pn", H, cin, cout, flags)
         if key not in self._ws_cache:
             f = getattr(self.ops, "conv_supported", None)
-            need = self._ws_need("c", H, cin, cout, False)
-            self._ws_cache[key] = bool(self.fuse_pixnorm and f is not None and
-                                       f(B=self.B, H=H, W=H, cin=cin, cout=cout,
-                                         flags=flags | L.CONV_PIXNORM | L.CONV_BIAS,
-                                         ws_bytes=need))
+            ok = bool(self.fuse_pixnorm and f is not None)
+            for b in self._GBs:   # the generator forward runs at B and, merged, at 2B
+                need = self._ws_need("c", H, cin, cout, False, b)
+                ok = ok and bool(f(B=b, H=H, W=H, cin=cin, cout=cout,
+                                   flags=flags | L.CONV_PIXNORM | L.CONV_BIAS, ws_bytes=need))
+            self._ws_cache[key] = ok
         return self._ws_cache[key]
 
     def _pnb_fused(self, H, cin, cout):
@@ -1288,17 +1315,41 @@ class StepEngine:
         X = D2["xin"]
         if before_fake is not None:
             before_fake()
-        img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
-        if self._low(alpha_D):
-            ops.img_fade(real, alpha_D, X[:B])                                   # :217-221
-        else:
-            X[:B].copy_(real)
+        z_g = self._z_g
+        self._z_g = None
+        if z_g is None:
+            img_fake = self.g_forward(PG, z, alpha_G, keep=False)               # :226-227
         trace, self.trace = self.trace, None
         try:
+            if z_g is not None:
+                # both generator forwards of the step in one (G is not updated in between):
+                # images [fake for D; fake for G] into X[B:3B], activations kept for the G half
+                g2 = self.g2
+                g2["z"][:B].copy_(z)
+                g2["z"][B:].copy_(z_g)
+                saved = self.g, self.B
+                self.g, self.B = g2, 2 * B
+                try:
+                    self.g_forward(PG, g2["z"], alpha_G, keep=True)             # :226-227, :244-245
+                finally:
+                    self.g, self.B = saved
+                self._g_done = True
+                img_fake = self.g["img"]
+            if self._low(alpha_D):
+                ops.img_fade(real, alpha_D, X[:B])                               # :217-221
+            else:
+                X[:B].copy_(real)
             with self._pair():
                 self.d_forward(PD, X, alpha_D)                                  # :216, :228
         finally:
             self.trace = trace
+        if trace is not None and z_g is not None:
+            trace("G", self)            # the D half's generator forward, then the G half's
+            self.g = self.g_hi
+            try:
+                trace("G", self)
+            finally:
+                self.g = self.g_lo
         h2 = self.h_mb
         self.h_mb = h2[:B]
         if trace is not None:   # one record per image, in the separate schedule's order
@@ -1388,7 +1439,20 @@ class StepEngine:
         ops, D, hp = self.ops, self.dd, self.hyper
         self._GG_flat.zero_()
         self.loss[3:4].zero_()
+        if self._g_done:
+            # the D half ran this half's generator forward (merged): its activations and
+            # image are the second half of the 2B generator buffers
+            self._g_done = False
+            self.g = self.g_hi
+            try:
+                return self._g_step_rest(PG, PD, GG, self.g["img"], alpha_G, alpha_D, before_d)
+            finally:
+                self.g = self.g_lo
         img = self.g_forward(PG, z, alpha_G)
+        return self._g_step_rest(PG, PD, GG, img, alpha_G, alpha_D, before_d)
+
+    def _g_step_rest(self, PG, PD, GG, img, alpha_G, alpha_D, before_d):
+        ops, D, hp = self.ops, self.dd, self.hyper
         if before_d is not None:
             before_d()
         self.d_forward(PD, img, alpha_D)
@@ -1463,8 +1527,13 @@ class StepEngine:
             self.pack("G", PG)
         if not self._packed["D"]:
             self.pack("D", PD)
+        # z2 for a merged generator forward (_d_step_merged): not with a bucketed DP exchange
+        # (grad_ready set), whose D all-reduce the G half's own generator forward hides
+        self._z_g = z2 if (self.g2 is not None and self.grad_ready is None) else None
         img_real, img_fake_D = self.d_step(PG, PD, fpD.gviews, real, z1, alpha_G, alpha_D,
                                            gp_eps=gp_eps, before_fake=self._finish_G)
+        if self._z_g is not None:   # d_step did not merge: the G half runs its own forward
+            self._z_g = None
         hD = grad_hook("D", fpD.live_grad()) if grad_hook is not None else None
 
         def finish_D():
