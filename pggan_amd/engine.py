@@ -1236,7 +1236,7 @@ class StepEngine:
         self.loss[:3].zero_()
         self.loss[4:5].zero_()
         if self._merged():
-            return self._d_step_merged(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake)
+            return self._d_step_merged(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake, gp_eps)
         conc = self.fstream is not None and hp.gp_mode == "r1"
         if conc:
             ev0 = torch.cuda.Event()   # the fake pass starts from here, beside the real part
@@ -1283,7 +1283,8 @@ class StepEngine:
         waiting for its DP exchange (that exchange overlaps the real-image part of the
         separate schedule, which does not read G; the merged forward needs the fake image
         first)."""
-        return (self.dd2 is not None and self.hyper.gp_mode == "r1" and self.fstream is None and
+        return (self.dd2 is not None and self.hyper.gp_mode in ("r1", "wgan-gp") and
+                self.fstream is None and
                 not hasattr(self._pending_G, "wait"))
 
     @contextlib.contextmanager
@@ -1296,7 +1297,7 @@ class StepEngine:
         finally:
             self.dd, self.B = saved
 
-    def _d_step_merged(self, PG, PD, GD, real, z, alpha_G, alpha_D, before_fake):
+    def _d_step_merged(self, PG, PD, GD, real, z, alpha_G, alpha_D, before_fake, gp_eps=None):
         """The R1 D half with the fake image's passes merged into the real image's
         (pggan/model.py:211-238; the same terms, batch [real; fake] = 2B):
           G forward (the fake image straight into the second half of the merged input),
@@ -1359,6 +1360,22 @@ class StepEngine:
                 trace("D", self)
             finally:
                 self.dd = D1
+        if hp.gp_mode != "r1":
+            # WGAN-GP mode: one backward over both halves from the two BCE terms (+ drift on
+            # the real half), then the penalty pass on the interpolation at batch B
+            ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], None)
+            if hp.W_drift:
+                ops.drift(D1["logit"], hp.W_drift, self.loss[4:5], D1["u"])   # pggan/loss.py:94-100
+            ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u"][B:], None)
+            self.h_mb = h2
+            try:
+                with self._pair():
+                    self.d_backward(PD, GD, D2["u"], alpha_D, img=X)
+            finally:
+                self.h_mb = h2[:B]
+            self._wgan_gp(PD, GD, X[:B], X[B:], gp_eps, alpha_D)
+            self._side_join()
+            return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
         ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], D1["hl"])    # lib/loss.py:119-123
         ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u2"][B:], None)
         gbar = self._input_grad(PD, D1["u"], alpha_D, "r1")                     # lib/loss.py:125-135
