@@ -29,6 +29,14 @@ from oracle import pggan_oracle as O
 # differ by 2%); the worst of 2e9 samples sits ~6-8 sigma out, measured 0.16.  A real
 # kernel error (a wrong sign far from 0) shows up at O(1) x RMS.
 FLIP_BOUND = {torch.float32: 2e-4, torch.bfloat16: 0.3}
+# Relative-error floor of gradient tensors that are a sum with heavy cancellation: the D
+# decision-layer bias gradient is ONE number, the sum over the batch of the logit gradients,
+# whose real (-(1 - sigma)/B) and fake (+sigma/B) terms nearly cancel once D is near
+# balance.  The fp32 GPU step (cross-workgroup fp32 atomics, run-to-run order) measured
+# 5.8e-4 - 1.02e-3 at tiny_s2_b8_a03 step 1 against the float64 oracle, with the separate and
+# the merged real/fake schedules alike (profiles/r4_merge_ab.txt); every other tensor stays
+# at the strict bar, and the CPU double at ~1e-6.
+CANCEL_TOL = {"D:decision_layer.module.bias": 2e-3}
 # bf16 only: at most this fraction of pre-activations may take the injected region
 # against the oracle's own sign (measured 0.15% at C5)
 FLIP_FRAC_BF16 = 1e-2
@@ -221,7 +229,8 @@ def compare(ours, ref, fpG, fpD, kinks, *, tol, flip_bound, ptol=None, what=""):
                     e = min(e, rel_l2(ours[key][n], ref[key + "_adam_ours"][n]))
                 errs[f"param {net}:{n}"] = e
     bad = {k: v for k, v in errs.items()
-           if v > (ptol if k.startswith("param") else tol) or not math.isfinite(v)}
+           if v > (ptol if k.startswith("param") else max(tol, CANCEL_TOL.get(k, 0.0)))
+           or not math.isfinite(v)}
     rep["errs"] = errs
     rep["worst"] = max(((k, v) for k, v in errs.items() if not k.startswith("param")),
                        key=lambda kv: kv[1])
