@@ -74,6 +74,18 @@ def test_engine_schedule_unfused_pixelnorm():
     run_and_check(meta, z, eng, fpG, fpD, tol=1e-3)
 
 
+@pytest.mark.parametrize("name", ["tiny_s3_b4_a1", "tiny_s1_b4_a05"])
+def test_engine_schedule_merged_generator_forward(name, monkeypatch):
+    """The opt-in merged generator forward (PG_MERGE_G=1: both G forwards of a step at
+    batch 2B, the G half reading the second-half views) against the golden fixtures."""
+    monkeypatch.setenv("PG_MERGE_G", "1")
+    torch.set_num_threads(4)
+    meta, z = load(name)
+    eng, fpG, fpD = build(meta, CpuOps())
+    assert eng.g2 is not None and eng.dd2 is not None
+    run_and_check(meta, z, eng, fpG, fpD, tol=1e-3)
+
+
 GP_NAMES = ["gp_tiny_s2_b8_a03", "gp_tiny_s1_b4_a05"]
 
 
