@@ -302,11 +302,8 @@ class StepEngine:
         # parameters (Adam_G runs after the G half): with merge_g they run as ONE forward at
         # batch 2B ([fake for D; fake for G], see _d_step_merged); the G buffers are
         # allocated at 2B, self.g holds first-half views and g_hi the G half's.
-        # Opt-in (PG_MERGE_G=1): +1.5 % at C5 (profiles/r4_merge_g_ab.txt), but one of two
-        # repeated bf16 runs at 256^2 (tools/elision_probe.py, profiles/r4_merge_g_ab.txt) gave a
-        # G-half loss and G gradient that differ from an identical run (same images, same D
-        # parameters) -- an ordering hazard not found yet, so it stays off by default.
-        merge_g = merge_d and os.environ.get("PG_MERGE_G", "0") == "1"
+        # PG_MERGE_G=0: separate forwards (A/B runs).  +1.5 % at C5 (profiles/r4_merge_g_ab.txt).
+        merge_g = merge_d and os.environ.get("PG_MERGE_G", "1") != "0"
         GB = 2 * B if merge_g else B
         self._GBs = (B, 2 * B) if merge_g else (B,)
         self._g_done = False
