@@ -58,6 +58,8 @@ def parse():
                    help="0: the process's CPU share (OMP_NUM_THREADS, else os.cpu_count())")
     p.add_argument("--gp-mode", choices=["r1", "wgan-gp"], default="r1")
     p.add_argument("--no-kernel-events", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step as a hipGraph from the second step on (one process)")
     p.add_argument("--dp-exchange", action="store_true",
                    help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
                         "group), to measure the bookkeeping's cost against the plain step")
@@ -101,13 +103,10 @@ class KernelTimer:
         # timing events without the system-scope fence (pg_event_create(timing=1)): a torch
         # timing event writes back and invalidates every XCD's L2 at each record, so the
         # launch it brackets would start cold and ~6.5 us late
-        if os.environ.get("PG_TORCH_EVENTS", "0") == "1":
-            self.ev = lambda: torch.cuda.Event(enable_timing=True)
-        else:
-            # created here, before any timed step: ~0.5k events per instrumented step, and
-            # creating them inside the step made the host the bottleneck of that step
-            pool = [ops.event(timing=True) for _ in range(2048)]
-            self.ev = lambda: pool.pop() if pool else ops.event(timing=True)
+        # created here, before any timed step: ~0.5k events per instrumented step, and
+        # creating them inside the step made the host the bottleneck of that step
+        pool = [ops.event(timing=True) for _ in range(2048)]
+        self.ev = lambda: pool.pop() if pool else ops.event(timing=True)
 
         def conv3x3(x, wpk, y, **kw):
             if not self.on:
@@ -306,6 +305,11 @@ def build_model(args, rank, local, world, ops_factory):
     return m
 
 
+def _engine_opts():
+    from pggan_amd import engine
+    return engine.engine_options()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -345,8 +349,9 @@ def main():
 
     log = lambda m: print(f"[bench] {m}", file=sys.stderr, flush=True)
     log(f"stage {s} batch {B} world {world}: {args.warmup} warm-up steps")
-    # PG_GRAPH=1 (one process): from the second step on, train_step replays the step
-    # captured as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
+    # --graph (one process): from the second step on, train_step replays the step captured
+    # as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
+    model.use_graph = bool(args.graph)
     for _ in range(args.warmup):
         step()
     model.flush()
@@ -493,9 +498,9 @@ def main():
                                    f"batch {B}/GPU, alpha {args.alpha}, depths {depths}" +
                                    (" (alpha = 1: the fade-in's zero-weight low-resolution "
                                     "branches elided, results bit-identical on the CPU double, "
-                                    "PG_ELIDE_BLEND=0 computes them)"
-                                    if args.alpha == 1.0 and os.environ.get("PG_ELIDE_BLEND", "1")
-                                    != "0" else ""),
+                                    "PG_ENGINE=elide_zero_blend=0 computes them)"
+                                    if args.alpha == 1.0 and
+                                    _engine_opts()["elide_zero_blend"] else ""),
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
             "host_enqueue_ms_per_step": round(host_ms, 3),

@@ -18,7 +18,10 @@
  *  - activations are NHWC with an explicit channel stride `*_cs` (elements);
  *    images at the API boundary are NCHW fp32 like the reference;
  *  - kernels are stateless and re-entrant; outputs are written fully unless an
- *    ACCUM flag / "accumulates" note says the result is added.
+ *    ACCUM flag / "accumulates" note says the result is added;
+ *  - results are deterministic: a call repeated on the same inputs and geometry gives
+ *    bitwise the same outputs (no order-dependent float atomics).  Sums over workgroups
+ *    go through a caller-provided `scratch` (PG_SCRATCH_BYTES, see below).
  */
 #ifndef PGGAN_HIP_H
 #define PGGAN_HIP_H
@@ -39,6 +42,16 @@ extern "C" {
 
 const char* pg_last_error(void);
 int pg_version(void);
+
+/* Reduction scratch of the entry points that sum over workgroups (the 1x1 RGB weight and bias
+ * gradients, the penalties' per-sample norms, pg_bias_grad, pg_r1_penalty, pg_gp_penalty): each
+ * workgroup stores its partial sums there and the last one to finish adds them in workgroup
+ * order (a fixed-order sum instead of float atomics), so results are bitwise reproducible.
+ * Contract: PG_SCRATCH_BYTES of device memory, zero-filled ONCE by the caller when allocated;
+ * one scratch per stream (calls on one stream may share it, calls that can run concurrently on
+ * different streams may not); every call returns it to its zero state. */
+#define PG_SCRATCH_BYTES (4u << 20)
+size_t pg_scratch_bytes(void);
 
 /* ---- equalized-LR 3x3 convolution (lib/layers.py:66-89, ConstrainedLayer.forward :58-63)
  * y = out_scale * post(conv3x3(pre(x), wpk) + bias)
@@ -143,7 +156,7 @@ int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const v
                         size_t ws_bytes, void* stream);
 /* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
-                 void* stream);
+                 void* scratch, void* stream);
 
 /* ---- PixelwiseVectorNorm (lib/layers.py:8-14) over the channel axis of NHWC */
 int pg_pixnorm_fwd(int dtype, int npix, int C, int cs, const void* x, void* y, void* stream);
@@ -182,7 +195,7 @@ int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const fl
 int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
                    float c, int Cp, int xp_cs, const void* xp, const float* wp, float cp,
                    float alpha, const float* gimg, void* gx, void* gxp, float* dw, float* db,
-                   float* dwp, float* dbp, void* stream);
+                   float* dwp, float* dbp, void* scratch, void* stream);
 /* fromRGB: y = lrelu(c*(W . img_in + b)), img_in = down ? avgpool2(img) : img  (img NCHW fp32);
  * R = output resolution.  b == NULL -> no bias; mask_y != NULL -> tangent mode:
  * y = c*(W . img_in) * lrelu'(mask_y) (no activation) */
@@ -200,7 +213,7 @@ int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, cons
  * dw[o][i] += c sum gz*img_in, db[o] += c sum gz (if dw/db) */
 int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
                     float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
-                    void* stream);
+                    void* scratch, void* stream);
 /* An image operand of the fromRGB layers given as a per-sample mix instead of a tensor:
  * img[b] = a[b] * x0[b] + c[b] * x1[b] (NCHW fp32; a, c: DEVICE arrays of B floats; x1 and c
  * may be NULL; a == NULL means img = x0).  The gradient-penalty passes read the interpolated
@@ -230,7 +243,8 @@ int pg_from_rgb_bits(int dtype, int B, int R, int C, const pg_img_src* img, int 
  * norms, fused into the pass that writes the input gradient) */
 int pg_from_rgb_bwd_src(int dtype, int B, int R, int C, const pg_img_src* img, int down,
                         const float* w, float c, int gz_cs, const void* gz, float* gimg,
-                        int gimg_overwrite, float* norms, float* dw, float* db, void* stream);
+                        int gimg_overwrite, float* norms, float* dw, float* db, void* scratch,
+                        void* stream);
 /* The penalty and the tangent-pass scale from the per-sample squared norms n_b of g = dD/dx:
  * mode 0 (R1, lib/loss.py:125-135): loss_out[0] += 0.5 * sum_b n_b / B, scale_b = 1 / B;
  * mode 1 (WGAN-GP, pggan/loss.py:81-87): loss_out[0] += w * sum_b (sqrt(n_b) - 1)^2,
@@ -298,14 +312,15 @@ int pg_bce_loss(int B, const float* logits, int target, float w, float* loss_out
  * and u_b += 2 w l_b (u: the logit gradient of the real-image BCE, accumulated) */
 int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u, void* stream);
 /* R1 = 0.5 * mean_b sum g^2 accumulated into r1_out[0]; gbar = g / B  (g: [n] fp32, B samples) */
-int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream);
+int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* scratch,
+                  void* stream);
 /* WGAN-GP optional mode (pggan/loss.py:54-92): interp = eps*xr + (1-eps)*xf (per-sample eps) */
 int pg_gp_interp(int B, size_t per, const float* xr, const float* xf, const float* eps,
                  float* out, void* stream);
 /* gp = w * sum_b (||g_b|| - 1)^2 -> gp_out[0] (accumulate); gbar_b = w*2*(||g_b||-1)/||g_b|| g_b;
  * norms[B] workspace */
 int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, float* norms,
-                  float* gbar, void* stream);
+                  float* gbar, void* scratch, void* stream);
 
 /* out = x + y*z (fp32; the R1 logit injection u + h*t, pggan/loss.py:16-27) */
 int pg_mul_add(size_t n, const float* x, const float* y, const float* z, float* out, void* stream);
@@ -359,17 +374,10 @@ int pg_event_create(int timing, void** ev);
 int pg_event_record(void* ev, void* stream);
 int pg_stream_wait_event(void* stream, void* ev);
 int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);
-/* Arm `ev` (NULL: disarm) for the next kernel this library launches on `stream` from this host
- * thread: that launch records the event at its completion (hipExtLaunchKernel's stop event), with
- * no marker packet of its own in the stream's queue -- hipEventRecord's marker delays the
- * stream's next kernel by ~6.5 us on MI355X.  pg_event_armed() is 1 while the event still waits
- * for its launch (then record it with pg_event_record). */
-int pg_event_arm(void* ev, void* stream);
 /* A non-blocking stream of the library's own; lowest_priority != 0: at the device's least
  * priority (its own hardware-queue pool, so never the queue of a normal-priority stream) */
 int pg_stream_create(int lowest_priority, void** stream);
 int pg_stream_destroy(void* stream);
-int pg_event_armed(void);
 int pg_event_destroy(void* ev);
 
 /* ---- step plan: the kernel path of every 3x3 conv pass (forward, input

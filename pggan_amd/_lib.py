@@ -83,10 +83,12 @@ class LinearDesc(ctypes.Structure):
 
 
 _lib = None
+_SIDE_STREAMS = {}   # device index -> the least-priority side stream (pg_stream_create)
 
 _VP, _I, _F, _SZ, _U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t, ctypes.c_uint64
 _SIGS = {
     "pg_version": ([], _I),
+    "pg_scratch_bytes": ([], _SZ),
     "pg_conv3x3_packed_elems": ([_I, _I, _I], _SZ),
     "pg_conv3x3_pack": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_conv3x3_pack_batch": ([_I, _I, _VP, _I, _VP], _I),
@@ -101,7 +103,7 @@ _SIGS = {
     "pg_conv3x3_wgrad_workspace_size": ([_I, ctypes.POINTER(ConvDesc)], _SZ),
     "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP],
                          _I),
-    "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP], _I),
+    "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd_y": ([_I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _VP], _I),
@@ -112,9 +114,9 @@ _SIGS = {
     "pg_rgb_out": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _I, _I, _VP, _VP, _VP, _F, _F, _VP,
                     _VP], _I),
     "pg_rgb_out_bwd": ([_I, _I, _I, _I, _I, _VP, _VP, _F, _I, _I, _VP, _VP, _F, _F, _VP, _VP,
-                        _VP, _VP, _VP, _VP, _VP, _VP], _I),
+                        _VP, _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_from_rgb": ([_I, _I, _I, _I, _VP, _I, _VP, _VP, _F, _F, _VP, _I, _VP, _VP], _I),
-    "pg_from_rgb_bwd": ([_I, _I, _I, _I, _VP, _I, _VP, _F, _I, _VP, _VP, _VP, _VP, _VP], _I),
+    "pg_from_rgb_bwd": ([_I, _I, _I, _I, _VP, _I, _VP, _F, _I, _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_img_fade": ([_I, _I, _I, _VP, _F, _VP, _VP], _I),
     "pg_from_rgb_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP, _I,
                          _VP, _VP], _I),
@@ -122,7 +124,7 @@ _SIGS = {
     "pg_from_rgb_bits": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP,
                           _I, _VP, _VP, _VP], _I),
     "pg_from_rgb_bwd_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _F, _I, _VP, _VP,
-                             _I, _VP, _VP, _VP, _VP], _I),
+                             _I, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_penalty_scale": ([_I, _I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_linear_fwd": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_linear_dgrad": ([_I, ctypes.POINTER(LinearDesc), _VP, _VP, _VP, _VP, _VP], _I),
@@ -136,10 +138,10 @@ _SIGS = {
     "pg_mbstd_bwd": ([_I, _I, _I, _I, _I, _VP, _I, _VP, _VP, _VP], _I),
     "pg_mbstd_r1": ([_I, _I, _I, _I, _I, _VP, _VP, _I, _VP, _VP, _VP, _VP], _I),
     "pg_bce_loss": ([_I, _VP, _I, _F, _VP, _VP, _VP, _VP], _I),
-    "pg_r1_penalty": ([_I, _SZ, _VP, _VP, _VP, _VP], _I),
+    "pg_r1_penalty": ([_I, _SZ, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_drift_loss": ([_I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_gp_interp": ([_I, _SZ, _VP, _VP, _VP, _VP, _VP], _I),
-    "pg_gp_penalty": ([_I, _SZ, _VP, _F, _VP, _VP, _VP, _VP], _I),
+    "pg_gp_penalty": ([_I, _SZ, _VP, _F, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_mul_add": ([_SZ, _VP, _VP, _VP, _VP, _VP], _I),
     "pg_adam": ([_SZ, _VP, _VP, _VP, _VP, _F, _F, _F, _F, _I, _VP], _I),
     "pg_randn": ([_SZ, _U64, _U64, _VP, _VP], _I),
@@ -160,10 +162,8 @@ _SIGS = {
     "pg_stream_wait_event": ([_VP, _VP], _I),
     "pg_event_elapsed_ms": ([_VP, _VP, ctypes.POINTER(ctypes.c_float)], _I),
     "pg_event_destroy": ([_VP], _I),
-    "pg_event_arm": ([_VP, _VP], _I),
     "pg_stream_create": ([_I, ctypes.POINTER(ctypes.c_void_p)], _I),
     "pg_stream_destroy": ([_VP], _I),
-    "pg_event_armed": ([], _I),
 }
 SYMBOLS = ["pg_last_error"] + list(_SIGS)
 
@@ -216,12 +216,6 @@ class HipEvent:
         if rc != 0:
             raise RuntimeError(f"stream_wait_event failed ({rc}): {self.lib.pg_last_error().decode()}")
 
-    def arm(self, stream=None):
-        """Record this event at the completion of the next kernel the library launches on
-        `stream` (default: current) from this thread (pg_event_arm)."""
-        s = stream if stream is not None else torch.cuda.current_stream()
-        self.lib.pg_event_arm(self.h, ctypes.c_void_p(s.cuda_stream))
-
     def elapsed_time(self, end):
         ms = ctypes.c_float()
         rc = self.lib.pg_event_elapsed_ms(self.h, end.h, ctypes.byref(ms))
@@ -246,10 +240,22 @@ class HipOps:
         assert dtype in (torch.float32, torch.bfloat16)
         self.tdtype = dtype
         self.dt = PG_F32 if dtype == torch.float32 else PG_BF16
+        self._scratch = {}   # stream handle -> reduction scratch (pg_scratch_bytes)
 
     # -- plumbing --------------------------------------------------------
     def _s(self):
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def _scr(self):
+        """The current stream's reduction scratch (include/pggan_hip.h: PG_SCRATCH_BYTES,
+        zero-filled once, one per stream; every call leaves it zeroed): the deterministic
+        fixed-order sums over workgroups of the RGB weight gradients, norms and biases."""
+        s = torch.cuda.current_stream()
+        t = self._scratch.get(s.cuda_stream)
+        if t is None:
+            n = int(self.lib.pg_scratch_bytes()) // 4
+            t = self._scratch[s.cuda_stream] = torch.zeros(n, dtype=torch.float32, device=s.device)
+        return _p(t)
 
     def _chk(self, rc, what):
         if rc != 0:
@@ -265,12 +271,17 @@ class HipOps:
         return PG_F32 if t.dtype == torch.float32 else PG_BF16
 
     # -- stream ordering -----------------------------------------------------
-    def stream(self, lowest_priority=False):
-        """A torch.cuda.ExternalStream over pg_stream_create (lives as long as the process)."""
-        h = ctypes.c_void_p()
-        self._chk(self.lib.pg_stream_create(int(bool(lowest_priority)), ctypes.byref(h)),
-                  "stream_create")
-        return torch.cuda.ExternalStream(h.value)
+    def side_stream(self):
+        """The current device's least-priority stream (pg_stream_create): created once per
+        process and device and shared by every engine (engines rebuilt per stage / batch
+        size reuse it instead of leaking a stream and its hardware queue each time)."""
+        dev = torch.cuda.current_device()
+        st = _SIDE_STREAMS.get(dev)
+        if st is None:
+            h = ctypes.c_void_p()
+            self._chk(self.lib.pg_stream_create(1, ctypes.byref(h)), "stream_create")
+            st = _SIDE_STREAMS[dev] = torch.cuda.ExternalStream(h.value)
+        return st
 
     def event(self, timing=False):
         """A HipEvent (device-scope release; see pg_event_create)."""
@@ -373,7 +384,7 @@ class HipOps:
         self._cuda(g, db)
         npix = g.numel() // g.shape[-1]
         self._chk(self.lib.pg_bias_grad(self._dt(g), npix, C, g.shape[-1], _p(g), scale, _p(db),
-                                        self._s()), "bias_grad")
+                                        self._scr(), self._s()), "bias_grad")
 
     # -- pixel norm ------------------------------------------------------
     def pixnorm(self, x, y, C):
@@ -437,7 +448,7 @@ class HipOps:
         self._chk(self.lib.pg_rgb_out_bwd(self._dt(x), B, R, C, x.shape[-1], _p(x), _p(w), c, Cp,
                                           xp.shape[-1] if xp is not None else 0, _p(xp), _p(wp), cp,
                                           alpha, _p(gimg), _p(gx), _p(gxp), _p(dw), _p(db), _p(dwp),
-                                          _p(dbp), self._s()), "rgb_out_bwd")
+                                          _p(dbp), self._scr(), self._s()), "rgb_out_bwd")
 
     def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope):
         """toRGB input gradient + the PixelNorm / LReLU backward of its input y (pg_rgb_out_bwd_pn)."""
@@ -484,7 +495,7 @@ class HipOps:
                                                ctypes.byref(src) if src is not None else None,
                                                1 if down else 0, _p(w), c, gz.shape[-1], _p(gz),
                                                _p(gimg), 1 if gimg_overwrite else 0, _p(norms),
-                                               _p(dw), _p(db), self._s()), "from_rgb_bwd")
+                                               _p(dw), _p(db), self._scr(), self._s()), "from_rgb_bwd")
 
     def penalty_scale(self, mode, norms, w, loss, scale):
         """mode "r1" / "wgan-gp": the penalty into loss[0] and the per-sample tangent scale
@@ -572,8 +583,8 @@ class HipOps:
 
     def r1_penalty(self, g, B, r1, gbar):
         self._cuda(g, r1, gbar)
-        self._chk(self.lib.pg_r1_penalty(B, g.numel(), _p(g), _p(r1), _p(gbar), self._s()),
-                  "r1_penalty")
+        self._chk(self.lib.pg_r1_penalty(B, g.numel(), _p(g), _p(r1), _p(gbar), self._scr(),
+                                         self._s()), "r1_penalty")
 
     def gp_interp(self, xr, xf, eps, out):
         self._cuda(xr, xf, eps, out)
@@ -585,7 +596,7 @@ class HipOps:
         self._cuda(g, gp, norms, gbar)
         B = g.shape[0]
         self._chk(self.lib.pg_gp_penalty(B, g.numel() // B, _p(g), w, _p(gp), _p(norms), _p(gbar),
-                                         self._s()), "gp_penalty")
+                                         self._scr(), self._s()), "gp_penalty")
 
     def mul_add(self, x, y, z, out):
         self._cuda(x, y, z, out)

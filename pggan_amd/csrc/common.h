@@ -145,6 +145,143 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// ---- deterministic cross-workgroup sums ------------------------------------
+// The reductions whose result sums over workgroups (the 1x1 RGB weight gradients, the
+// per-sample squared norms of the penalties, the bias gradient) used fp32 atomics: the order of
+// the adds followed the order the workgroups finished, so two runs of the same step differed in
+// the last bits (and a bf16 rounding downstream could amplify that, tools/repro_probe.py).
+// Instead every workgroup stores its totals into the caller's scratch (pg_scratch_bytes, one per
+// stream, zero-filled once) and the last workgroup to arrive sums them in workgroup order with a
+// fixed split over its threads: the result depends only on the launch geometry.
+// Hand-off (MI355X guide, in-launch split-K recipe): plain partial stores -> vmcnt(0) -> barrier
+// -> one lane's agent-scope release -> vmcnt(0) -> relaxed agent ticket; the drawer of the last
+// ticket acquires (agent) before reading the partials, and returns the ticket to 0.
+constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
+__host__ __device__ constexpr size_t pg_scratch_floats() {
+  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
+}
+
+// Every thread of every workgroup calls this last, uniformly.  tot: LDS, the workgroup's NA
+// totals (visible to all threads: a __syncthreads() after writing them); tmp: LDS scratch of
+// >= max(NA, 4 * blockDim.x) floats, may alias tot.  fin(q, total) runs once per q < NA in the
+// last workgroup (the sum over workgroups 0..nb-1 in order, as groups of consecutive workgroups
+// summed in group order).  nb * NA <= pg_scratch_floats() (checked by the host).
+template <typename Fin>
+__device__ __forceinline__ void det_commit(const float* tot, int NA, float* scratch, float* tmp,
+                                           Fin fin) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+  const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
+  float* part = scratch + PG_SCRATCH_HDR_FLOATS;
+  for (int q = tid; q < NA; q += nt) part[(size_t)bid * NA + q] = tot[q];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned det_last;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    det_last = (t == nb - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!det_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // G groups of consecutive workgroups per output; items (q, g) spread over the threads
+  int G = (4 * nt) / (NA > 0 ? NA : 1);
+  G = G < 1 ? 1 : G > 64 ? 64 : G;
+  if ((unsigned)G > nb) G = (int)nb;
+  const unsigned per = (nb + G - 1) / G;
+  for (int it = tid; it < NA * G; it += nt) {
+    const int q = it % NA, g = it / NA;
+    const unsigned b0 = g * per, b1 = b0 + per < nb ? b0 + per : nb;
+    float s = 0.f;
+    unsigned b = b0;
+    for (; b + 8 <= b1; b += 8) {   // 8 loads in flight, summed in workgroup order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u) * NA + q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < b1; ++b) s += part[(size_t)b * NA + q];
+    tmp[it] = s;
+  }
+  __syncthreads();
+  for (int q = tid; q < NA; q += nt) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += tmp[g * NA + q];
+    fin(q, s);
+  }
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Segmented form: each workgroup contributes ONE value `v` (valid in thread 0) to output
+// q = bid / (nb / nseg) (the workgroups of one output are a contiguous index range, e.g. the
+// blocks of one sample); fin(q, total) for q < nseg in the last workgroup.  tmp: LDS of
+// >= 4 * blockDim.x floats.  nb <= pg_scratch_floats(), nb % nseg == 0.
+template <typename Fin>
+__device__ __forceinline__ void det_commit_seg(float v, int nseg, float* scratch, float* tmp,
+                                               Fin fin) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+  const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
+  float* part = scratch + PG_SCRATCH_HDR_FLOATS;
+  if (tid == 0) part[bid] = v;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned det_last;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    det_last = (t == nb - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!det_last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const unsigned seg = nb / nseg;
+  int G = (4 * nt) / nseg;
+  G = G < 1 ? 1 : G > 64 ? 64 : G;
+  if ((unsigned)G > seg) G = (int)seg;
+  const unsigned per = (seg + G - 1) / G;
+  for (int it = tid; it < nseg * G; it += nt) {
+    const int q = it % nseg, g = it / nseg;
+    const unsigned j0 = g * per, j1 = j0 + per < seg ? j0 + per : seg;
+    const float* p = part + (size_t)q * seg;
+    float s = 0.f;
+    unsigned j = j0;
+    for (; j + 8 <= j1; j += 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = p[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += w[u];
+    }
+    for (; j < j1; ++j) s += p[j];
+    tmp[it] = s;
+  }
+  __syncthreads();
+  for (int q = tid; q < nseg; q += nt) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += tmp[g * nseg + q];
+    fin(q, s);
+  }
+  if (tid == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// host side: whether a launch of nb workgroups with na partials each fits the scratch
+static inline bool pg_det_fits(size_t nb, size_t na) { return nb * na <= pg_scratch_floats(); }
+
 // ---- error plumbing -------------------------------------------------------
 void pg_set_error(const char* fmt, ...);
 
@@ -156,20 +293,8 @@ void pg_set_error(const char* fmt, ...);
     }                                       \
   } while (0)
 
-// Every kernel launch of the library goes through PG_KLAUNCH: a launch on the stream an event
-// was armed for (pg_event_arm) records that event at the kernel's completion
-// (hipExtLaunchKernelGGL's stop event, no marker packet of its own in the queue); every other
-// launch is a plain hipLaunchKernelGGL.
-hipEvent_t pg_take_armed_event(hipStream_t s);
-#define PG_KLAUNCH(K, G, B, L, S, ...)                                                     \
-  do {                                                                                    \
-    hipStream_t pgks_ = (S);                                                              \
-    hipEvent_t pgke_ = pg_take_armed_event(pgks_);                                        \
-    if (pgke_)                                                                            \
-      hipExtLaunchKernelGGL(K, G, B, L, pgks_, nullptr, pgke_, 0, __VA_ARGS__);           \
-    else                                                                                  \
-      hipLaunchKernelGGL(K, G, B, L, pgks_, __VA_ARGS__);                                 \
-  } while (0)
+// Every kernel launch of the library goes through PG_KLAUNCH.
+#define PG_KLAUNCH(K, G, B, L, S, ...) hipLaunchKernelGGL(K, G, B, L, (S), __VA_ARGS__)
 
 #define PG_LAUNCH_CHECK()                                                       \
   do {                                                                          \

@@ -632,8 +632,9 @@ __global__ void conv_splitk_epilogue(ConvParams p, int splits) {
 // --------------------------------------------------------------------------
 // Weight gradient: dW[o][c][tap] += scale * sum_p gz[p][o] * x[p + off(tap)][c]
 // One workgroup = 32 output channels x 32 input channels x 9 taps, walking a
-// contiguous range of spatial pixel tiles (split over blockIdx.z); partial
-// sums are added with fp32 atomics.  MFMA v_mfma_f32_16x16x4_f32 with
+// contiguous range of spatial pixel tiles (split over blockIdx.z); each split writes
+// its partial sums to a workspace slab (summed in slab order by wgrad_slab_reduce), or, with
+// one split, adds them to dw directly.  MFMA v_mfma_f32_16x16x4_f32 with
 // K = pixels: A[o][p] and B[p][c] are one ds_read_b32 each from the
 // pixel-major LDS tiles (exact fp32; bf16 inputs are widened on staging).
 // --------------------------------------------------------------------------
@@ -642,6 +643,8 @@ struct WgParams {
   const void* gz;
   float* dw;
   float* db;
+  float* ws;       // split slabs [splits][cout*cin*9 + cout], or NULL (one split: direct)
+  size_t slab;
   int B, H, W, Hin, Win;
   int cin, cout, x_cs, gz_cs;
   int ups;
@@ -718,18 +721,44 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
       }
     }
   }
-  if (do_db && o0 + tid < p.cout) atomicAdd(p.db + o0 + tid, bsum * p.scale);
+  float* slab = p.ws ? p.ws + blockIdx.z * p.slab : nullptr;
+  if (do_db && o0 + tid < p.cout) {
+    if (slab) slab[(size_t)p.cout * p.cin * 9 + o0 + tid] = bsum;
+    else p.db[o0 + tid] += bsum * p.scale;   // one split: the sole writer
+  }
   // acc[tap][j]: row (o) = om + 4g + j, col (c) = cn + r
   const int c = cc0 + cn + r;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = o0 + om + 4 * g + j;
     if (o < p.cout && c < p.cin) {
-      float* dst = p.dw + ((size_t)o * p.cin + c) * 9;
+      const size_t e = ((size_t)o * p.cin + c) * 9;
+      if (slab) {
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) atomicAdd(dst + tap, acc[tap][j] * p.scale);
+        for (int tap = 0; tap < 9; ++tap) slab[e + tap] = acc[tap][j];
+      } else {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) p.dw[e + tap] += acc[tap][j] * p.scale;
+      }
     }
   }
+}
+
+// the fp32 weight gradient's split of the pixel tiles (enough workgroups to fill the chip)
+static int wgrad_f32_splits(const pg_conv_desc* d, int* tiles_per_split) {
+  TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
+  const int ntiles = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH);
+  const int ot = pg_cdiv(d->cout, WG_BO), ct = pg_cdiv(d->cin, WG_BC);
+  int splits = pg_cdiv(2048, ot * ct);
+  if (splits > ntiles) splits = ntiles;
+  if (splits < 1) splits = 1;
+  *tiles_per_split = pg_cdiv(ntiles, splits);
+  return pg_cdiv(ntiles, *tiles_per_split);
+}
+static size_t wgrad_f32_ws_bytes(const pg_conv_desc* d) {
+  int tps;
+  const int splits = wgrad_f32_splits(d, &tps);
+  return splits > 1 ? (size_t)splits * ((size_t)d->cout * d->cin * 9 + d->cout) * sizeof(float) : 0;
 }
 
 // --------------------------------------------------------------------------
@@ -749,8 +778,9 @@ __global__ __launch_bounds__(256) void wgrad3x3_kernel(WgParams p) {
 // Reduction over pixel splits (blockIdx.z), chosen on the host:
 //   WG_DIRECT : one split -> plain coalesced read-modify-write of dw / db
 //   WG_SLABS  : split z writes an fp32 partial slab of the workspace; a second
-//               kernel sums the slabs into dw / db (few, spread atomics)
-//   WG_ATOMIC : no workspace given -> fp32 atomics per (o, c, tap) per split
+//               kernel sums the slabs into dw / db in slab order
+// (no workspace for the slabs -> the plan falls back to one split: results never depend on
+// the order workgroups finish)
 // Writes go through a per-wave LDS transpose so that each wave instruction covers
 // contiguous [c][tap] runs of one OIHW row.
 // --------------------------------------------------------------------------
@@ -763,7 +793,7 @@ __device__ __forceinline__ bf16x8_t tr_read8(const bf16_t* lo, const bf16_t* hi)
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-enum { WG_DIRECT = 0, WG_SLABS = 1, WG_ATOMIC = 2 };
+enum { WG_DIRECT = 0, WG_SLABS = 1 };
 
 struct WgBParams {
   const bf16_t* x;
@@ -1115,7 +1145,7 @@ void wgrad_bf16_kernel(WgBParams p) {
       v[k2] = sum;
       offs[k2] = (o < p.cout && c < p.cin) ? (o * p.cin + c) * 9 + tap : -1;
     }
-    if (p.mode == WG_DIRECT || p.mode == WG_ATOMIC) {
+    if (p.mode == WG_DIRECT) {
       // one fp32 add per element into dW.  WG_DIRECT: this workgroup is the only writer in
       // the launch, so the (no-return, fire-and-forget) atomic performs the same single
       // add old + v*scale as a read-modify-write, without a dependent load round trip per
@@ -1131,30 +1161,36 @@ void wgrad_bf16_kernel(WgBParams p) {
   }
 }
 
-// Sum the split slabs: block (x, y) adds slabs [y*spb, (y+1)*spb) of 256 consecutive
-// outputs; one atomic per output per y (plain read-modify-write when gridDim.y == 1).
+// Sum the split slabs (slab order, deterministic): block x covers 64 consecutive outputs with
+// 4 slab groups (a wave each: 256 contiguous bytes of one slab per load); wave g sums slabs
+// [g*spg, (g+1)*spg) with 4 loads in flight, the 4 group sums are added in group order through
+// LDS and added once to dw / db.  (The former 2-D grid added its y-partials with fp32 atomics:
+// order-dependent results, tools/repro_probe.py.)
 __global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t slab, int splits,
-                                                         int spb, int nw, float* dw, float* db,
-                                                         float scale) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= slab) return;
-  const int s0 = blockIdx.y * spb, s1 = min(splits, s0 + spb);
+                                                         int nw, float* dw, float* db, float scale) {
+  __shared__ float part[4][64];
+  const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + l;
+  const int spg = (splits + 3) / 4;
+  const int s0 = g * spg, s1 = min(splits, s0 + spg);
   float s = 0.f;
-  int k = s0;
-  for (; k + 4 <= s1; k += 4) {   // 4 loads in flight per round, summed in slab order
-    float t[4];
+  if (i < slab) {
+    int k = s0;
+    for (; k + 4 <= s1; k += 4) {   // 4 loads in flight per round, summed in slab order
+      float t[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) t[u] = ws[(size_t)(k + u) * slab + i];
+      for (int u = 0; u < 4; ++u) t[u] = ws[(size_t)(k + u) * slab + i];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s += t[u];
+      for (int u = 0; u < 4; ++u) s += t[u];
+    }
+    for (; k < s1; ++k) s += ws[(size_t)k * slab + i];
   }
-  for (; k < s1; ++k) s += ws[(size_t)k * slab + i];
+  part[g][l] = s;
+  __syncthreads();
+  if (g != 0 || i >= slab) return;
+  const float t = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
   float* dst = i < (size_t)nw ? dw + i : (db ? db + (i - nw) : nullptr);
-  if (!dst) return;
-  if (gridDim.y == 1)
-    *dst += s * scale;
-  else
-    atomicAdd(dst, s * scale);
+  if (dst) *dst += t * scale;
 }
 
 // The same sum, thread = 4 consecutive outputs: one 16-byte load per slab, RSP of them issued
@@ -1203,27 +1239,17 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   pl.WMO = 1;
   // two 16-channel halves of a 32-channel input slice per workgroup (waves split the
   // channels, the gz tile is staged once for both): A/B -5..-22 % at 32^2-256^2 for
-  // cin > 32; below 32^2 the single-half tile is faster
-  // PG_WG_DMA16=1: the 16^2 wide layers on wgrad_dma_kernel too (it needs WNC = 2); measured
-  // 28.6 vs 24.1 us for the register-staged single-half tile at 16^2 512 -> 512, so off
-  const char* dma16_env = getenv("PG_WG_DMA16");   // per call: the op tests switch it
-  const int dma16 = dma16_env ? atoi(dma16_env) : 0;
-  const bool w16_dma = dma16 && d->W == 16 && d->H % 8 == 0 && co % 64 == 0 && ci % 32 == 0 &&
-                       !(d->flags & PG_CONV_GZ_BITS);
-  pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32 || w16_dma) ? 2 : 1;
+  // cin > 32; below 32^2 the single-half tile is faster (the LDS-DMA kernel, which needs
+  // WNC = 2, measured 28.6 vs 24.1 us at 16^2 512 -> 512)
+  pl.WNC = ci <= 16 ? 1 : (ci <= 32 || d->W >= 32) ? 2 : 1;
   // ... unless the single-half tiles overflow one round of workgroups (the 513-channel
   // minibatch-stddev conv at 4^2: 8 x 33 = 264 > 256 ran as two rounds, 29.6 us vs 15.8)
   if (pl.WNC == 1 && ci > 16 && pg_cdiv(co, co <= 16 ? 16 : co <= 32 ? 32 : 64) * pg_cdiv(ci, 16) > 256)
     pl.WNC = 2;
-  if (const char* e = getenv("PG_WG_WNC")) { if (ci > 16) pl.WNC = atoi(e); }   // tuning runs only
   const int BO = pl.WMO * pl.MO * 16, BC = pl.WNC * pl.NC * 16;
-  // A/B (tools/wgbp_ab.sh): 256-pixel tiles -6..-10 % at 32^2-128^2 for the single-half
-  // (WNC = 1) tile, but the two-half tile is faster still there (tools/wnc_sweep.sh), so
-  // the default never picks them; PG_WG_BP=256 for tuning; +50 % with WNC = 2 (spills)
-  const bool bp256_ok = pl.MO >= 4 && pl.WNC == 1 && d->W >= 32 && d->H >= 32 && d->W <= 128 &&
-                        !(d->flags & PG_CONV_GZ_BITS);
-  pl.BP = bp256_ok ? 256 : WGB_BP;
-  if (const char* e = getenv("PG_WG_BP")) pl.BP = (atoi(e) == 256 && bp256_ok) ? 256 : 128;   // tuning
+  // 128-pixel tiles (256-pixel ones measured -6..-10 % for the single-half tile at 32^2-128^2,
+  // where the two-half tile is faster still, and +50 % with two halves: spills)
+  pl.BP = WGB_BP;
   pl.tc = pick_tile(d->H, d->W, pl.BP, 32);
   pl.ntiles = pg_cdiv(d->B, pl.tc.NB) * (d->W / pl.tc.TW) * (d->H / pl.tc.TH);
   pl.ot = pg_cdiv(co, BO);
@@ -1246,9 +1272,6 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
       else if (pl.MO == 1 && pl.WNC == 1) target = 1024;
     }
   }
-  if (const char* e = getenv("PG_WG_TARGET")) target = atoi(e);   // tuning runs only
-  if (const char* e = getenv("PG_WG_TARGET_NARROW")) { if (pl.MO < 4) target = atoi(e); }   // A/B
-  if (const char* e = getenv("PG_WG_TARGET_WIDE")) { if (pl.MO >= 4) target = atoi(e); }     // A/B
   int splits = base >= 256 ? 1 : pg_cdiv(target, base);
   const int max_splits = pl.ntiles / 2 > 1 ? pl.ntiles / 2 : 1;
   if (splits > max_splits) splits = max_splits;
@@ -1268,21 +1291,15 @@ size_t wgrad_bf16_ws_bytes(const pg_conv_desc* d) {
 int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const float* ws, float* dw,
                       float* db, float scale, hipStream_t st) {
   if (mode != WG_SLABS) return PG_OK;
-  static const int red4 = getenv("PG_WG_RED4") ? atoi(getenv("PG_WG_RED4")) : 1;   // A/B switch
-  if (red4 && pl.slab >= 65536 && pl.slab % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
+  if (pl.slab >= 65536 && pl.slab % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
     // wide layers (>= 256 blocks of 64 threads): vector form, one thread sums every split
     PG_KLAUNCH(wgrad_slab_reduce4, dim3((unsigned)pg_cdiv((long long)pl.slab / 4, 64)), dim3(64), 0, st,
                        ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
     PG_LAUNCH_CHECK();
     return PG_OK;
   }
-  const int nblk = (int)pg_cdiv((long long)pl.slab, 256);
-  int ry = pg_cdiv(512, nblk);
-  if (ry > pl.splits) ry = pl.splits;
-  const int spb = pg_cdiv(pl.splits, ry);
-  ry = pg_cdiv(pl.splits, spb);
-  PG_KLAUNCH(wgrad_slab_reduce, dim3(nblk, ry), dim3(256), 0, st, ws, pl.slab, pl.splits, spb,
-                     d->cout * d->cin * 9, dw, db, scale);
+  PG_KLAUNCH(wgrad_slab_reduce, dim3((unsigned)pg_cdiv((long long)pl.slab, 64)), dim3(256), 0, st,
+                     ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1320,22 +1337,18 @@ int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, c
   p.gzb = (d->flags & PG_CONV_GZ_BITS) ? reinterpret_cast<const unsigned char*>(gzbits) : nullptr;
   p.gzb_cs = d->xb_cs;
   p.slope = d->slope;
-  static const int xcd = getenv("PG_WG_XCD") ? atoi(getenv("PG_WG_XCD")) : 1;   // A/B switch
-  p.xcd_remap = xcd;
+  p.xcd_remap = 1;
   PG_CHECK_ARG(!p.gzb || (d->xb_cs * 8 >= d->cout && pl.tc.TH % 2 == 0 && pl.tc.TW % 2 == 0),
                "wgrad_bf16: GZ_BITS needs gzbits with >= cout/8 bytes per pixel");
   PG_CHECK_ARG(pl.BP == BP && p.halo_elems <= wgb_maxhalo(BP), "wgrad_bf16: halo %d > %d", p.halo_elems,
                wgb_maxhalo(BP));
   p.slab = pl.slab;
   p.ws = nullptr;
-  if (pl.splits == 1) {
-    p.mode = WG_DIRECT;
-  } else if (ws && ws_bytes >= pl.splits * pl.slab * sizeof(float)) {
-    p.mode = WG_SLABS;
-    p.ws = ws;
-  } else {
-    p.mode = WG_ATOMIC;
-  }
+  // wgrad_bf16_dispatch re-plans to one split when the workspace cannot hold the slabs
+  PG_CHECK_ARG(pl.splits == 1 || (ws && ws_bytes >= pl.splits * pl.slab * sizeof(float)),
+               "wgrad: split plan without its workspace");
+  p.mode = pl.splits == 1 ? WG_DIRECT : WG_SLABS;
+  if (p.mode == WG_SLABS) p.ws = ws;
   // + 16 B: store_tile's scratch slot behind the halo
   int lds = (BP * p.GZS + (BP / 8) * 64 + p.halo_elems * p.HS + (p.halo_elems / 8 + 1) * p.hpad) * 2 + 16;
   const int need = 4 * 9 * 64 * 4 * 4;   // epilogue dump of one (mo, nc) block per wave
@@ -1361,11 +1374,14 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS) || gzbits, "wgrad_bf16: GZ_BITS without gzbits");
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
-  const WgbPlan pl = wgrad_bf16_plan(d);
+  WgbPlan pl = wgrad_bf16_plan(d);
+  if (pl.splits > 1 && !(ws && ws_bytes >= pl.splits * pl.slab * sizeof(float))) {
+    pl.splits = 1;   // no room for the slabs: one split (WG_DIRECT), deterministic
+    pl.tiles_per_split = pl.ntiles;
+  }
   if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits);
-  // (prefetch depth, waves per SIMD); PG_WG_VARIANT="pd,wpe" overrides for tuning runs
-  int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
-  if (const char* e = getenv("PG_WG_VARIANT")) sscanf(e, "%d,%d", &pd, &wpe);
+  // (prefetch depth, waves per SIMD) from the round-1 sweep
+  const int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   const bool gzb = (d->flags & PG_CONV_GZ_BITS) != 0;
 #define PG_WGB(a, b, c, e, PD, WPE)                                                        \
   if (pl.MO == a && pl.NC == b && pl.WMO == c && pl.WNC == e && pd == PD && wpe == WPE) {  \
@@ -1373,12 +1389,6 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
       if (gzb)                                                                             \
         return launch_wgrad_bf16<a, b, c, e, PD, WPE, true>(d, pl, x, gz, scale, dw, db,   \
                                                             ws, ws_bytes, st, gzbits);     \
-    }                                                                                      \
-    if constexpr (a == 4) {                                                                \
-      if (pl.BP == 256 && !gzb)                                                            \
-        return launch_wgrad_bf16<a, b, c, e, PD, WPE, false, 256>(d, pl, x, gz, scale, dw, \
-                                                                  db, ws, ws_bytes, st,    \
-                                                                  gzbits);                 \
     }                                                                                      \
     PG_CHECK_ARG(!gzb, "wgrad_bf16: GZ_BITS not instantiated for this tile");              \
     return launch_wgrad_bf16<a, b, c, e, PD, WPE, false>(d, pl, x, gz, scale, dw, db, ws,  \
@@ -1388,15 +1398,7 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
   PG_WGB(1, 1, 1, 2, 2, 2)
   PG_WGB(2, 1, 1, 1, 2, 2)
   PG_WGB(2, 1, 1, 2, 2, 2)
-  PG_WGB(2, 1, 1, 2, 2, 1)
-  PG_WGB(2, 1, 1, 2, 1, 2)
-  PG_WGB(4, 1, 1, 1, 1, 2)
-  PG_WGB(4, 1, 1, 1, 2, 2)
-  PG_WGB(4, 1, 1, 1, 2, 1)
   PG_WGB(4, 1, 1, 1, 4, 1)
-  PG_WGB(4, 1, 1, 2, 1, 2)
-  PG_WGB(4, 1, 1, 2, 2, 2)
-  PG_WGB(4, 1, 1, 2, 2, 1)
   PG_WGB(4, 1, 1, 2, 4, 1)
 #undef PG_WGB
   PG_CHECK_ARG(false, "wgrad_bf16: no kernel for plan");
@@ -1484,10 +1486,12 @@ __global__ __launch_bounds__(256) void pack_batch_kernel(const pg_pack_item* ite
     it.bias_scaled[o0 + tid] = it.bias ? it.bias[o0 + tid] * it.scale : 0.f;
 }
 
+// db[c] += scale * sum_p g[p][c]: block totals summed over blocks in block order (det_commit)
 template <typename T>
-__global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scale, float* db,
-                                 int pix_per_block) {
+__global__ __launch_bounds__(256) void bias_grad_kernel(int npix, int C, int cs, const T* g, float scale,
+                                                        float* db, int pix_per_block, float* scratch) {
   __shared__ float red[256];
+  __shared__ float tot[1024];   // C <= 1024 totals, then det_commit's tmp
   const int p0 = blockIdx.x * pix_per_block;
   const int p1 = min(npix, p0 + pix_per_block);
   if (C <= 256 && (256 % C) == 0) {
@@ -1500,15 +1504,17 @@ __global__ void bias_grad_kernel(int npix, int C, int cs, const T* g, float scal
     if (threadIdx.x < C) {
       float t = 0.f;
       for (int q = 0; q < ppi; ++q) t += red[q * C + threadIdx.x];
-      atomicAdd(db + threadIdx.x, t * scale);
+      tot[threadIdx.x] = t;
     }
   } else {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       float s = 0.f;
       for (int pp = p0; pp < p1; ++pp) s += Ty<T>::ld(g + (size_t)pp * cs + c);
-      atomicAdd(db + c, s * scale);
+      tot[c] = s;
     }
   }
+  __syncthreads();
+  det_commit(tot, C, scratch, tot, [&](int c, float t) { db[c] += t * scale; });
 }
 
 void conv_tile_for(int cout, int* BM, int* BN, int W = 16) {
@@ -1528,12 +1534,7 @@ int conv_splits(const pg_conv_desc* d) {
   const int base = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH) * pg_cdiv(cout_p, BN);
   const int cin_p = cinp_of(d->cin);
   const int nch = cin_p / (cin_p < 32 ? cin_p : 32);
-  // PG_CONV_SPLIT="min_base,target" overrides for tuning runs
-  static int min_base = -1, target = 256;
-  if (min_base < 0) {
-    min_base = 128;
-    if (const char* e = getenv("PG_CONV_SPLIT")) sscanf(e, "%d,%d", &min_base, &target);
-  }
+  constexpr int min_base = 128, target = 256;   // round-2 split sweep
   if (base >= min_base || nch < 4) return 1;
   int sp = pg_cdiv(target, base);
   if (sp > nch) sp = nch;
@@ -1596,8 +1597,7 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   p.ws = splits > 1 ? (float*)ws : nullptr;
   p.cps = pg_cdiv(p.nchunks, splits);
   p.slab = (size_t)d->B * d->H * d->W * p.cout_p;
-  static const int xcd = getenv("PG_CONV_XCD") ? atoi(getenv("PG_CONV_XCD")) : 1;   // A/B switch
-  p.xcd_remap = xcd;
+  p.xcd_remap = 1;
   dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
             splits);
   PG_LDS_ATTR((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), 160 * 1024);
@@ -1644,12 +1644,6 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 #include "conv_lr.inc"
 #include "wgrad_dma.inc"
 
-}  // namespace
-// the K-grouped wide conv (conv_kg.hip)
-bool conv_kg_ok(const pg_conv_desc* d);
-int conv_kg_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias, const void* aux,
-                     void* y, void* y2, hipStream_t st);
-namespace {
 
 // Which fused epilogues the kernel the dispatcher picks supports.
 template <typename T>
@@ -1694,7 +1688,6 @@ int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const f
                d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
     if (conv_lr_ok(d)) return conv_lr_dispatch(d, x, wpk, bias, aux, y, y2, st);
-    if (conv_kg_ok(d)) return conv_kg_dispatch(d, x, wpk, bias, aux, y, y2, st);
     if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, xbits, st);
   }
   int BM, BN;
@@ -1822,7 +1815,8 @@ int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes) {
 }
 
 size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d) {
-  return (d && dtype == PG_BF16) ? wgrad_bf16_ws_bytes(d) : 0;
+  if (!d) return 0;
+  return dtype == PG_BF16 ? wgrad_bf16_ws_bytes(d) : wgrad_f32_ws_bytes(d);
 }
 
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
@@ -1846,11 +1840,15 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
   p.tiles_y = d->H / tc.TH;
   p.ntiles = pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y;
   const int ot = pg_cdiv(d->cout, WG_BO), ct = pg_cdiv(d->cin, WG_BC);
-  int splits = pg_cdiv(2048, ot * ct);
-  if (splits > p.ntiles) splits = p.ntiles;
-  if (splits < 1) splits = 1;
-  p.tiles_per_split = pg_cdiv(p.ntiles, splits);
-  splits = pg_cdiv(p.ntiles, p.tiles_per_split);
+  int splits = wgrad_f32_splits(d, &p.tiles_per_split);
+  p.slab = (size_t)d->cout * d->cin * 9 + d->cout;
+  p.ws = nullptr;
+  if (splits > 1 && ws && ws_bytes >= splits * p.slab * sizeof(float)) {
+    p.ws = (float*)ws;
+  } else {   // no room for the slabs: one split (deterministic, slower)
+    splits = 1;
+    p.tiles_per_split = p.ntiles;
+  }
   const int lds = (WG_BP * WG_RS + tc.NB * (tc.TH + 2) * (tc.TW + 2) * WG_RS) * 4;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(ot, ct, splits);
@@ -1858,6 +1856,9 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
     PG_KLAUNCH(wgrad3x3_kernel<float>, grid, dim3(256), lds, st, p);
   else
     PG_KLAUNCH(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
+  if (p.ws)
+    PG_KLAUNCH(wgrad_slab_reduce, dim3((unsigned)pg_cdiv((long long)p.slab, 64)), dim3(256), 0, st,
+                       p.ws, p.slab, splits, d->cout * d->cin * 9, dw, db, scale);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1875,22 +1876,25 @@ int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const v
 }
 
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
-                 void* stream) {
-  PG_CHECK_ARG(g && db && npix > 0 && C > 0 && cs >= C, "bias_grad: bad args");
+                 void* scratch, void* stream) {
+  PG_CHECK_ARG(g && db && npix > 0 && C > 0 && C <= 1024 && cs >= C && scratch,
+               "bias_grad: bad args (C <= 1024, scratch required)");
   int ppb = 256;
   int blocks = pg_cdiv(npix, ppb);
-  if (blocks > 2048) {
-    blocks = 2048;
+  int cap = (int)(pg_scratch_floats() / (size_t)C);
+  if (cap > 2048) cap = 2048;
+  if (blocks > cap) {
+    blocks = cap;
     ppb = pg_cdiv(npix, blocks);
     blocks = pg_cdiv(npix, ppb);
   }
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32)
     PG_KLAUNCH(bias_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
-                       (const float*)g, scale, db, ppb);
+                       (const float*)g, scale, db, ppb, (float*)scratch);
   else
     PG_KLAUNCH(bias_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, npix, C, cs,
-                       (const bf16_t*)g, scale, db, ppb);
+                       (const bf16_t*)g, scale, db, ppb, (float*)scratch);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1905,8 +1909,7 @@ namespace {
 struct PlanLayer {
   char net, kind[8];
   int H, cin, cout, ups;
-  int fwd_path, dgrad_path;   // 0 conv3x3 (split-K when ws > 0), 1 conv_hr tile t, 2 conv_lr,
-                              // 3 conv_kg
+  int fwd_path, dgrad_path;   // 0 conv3x3 (split-K when ws > 0), 1 conv_hr tile t, 2 conv_lr
   int fwd_tile, dgrad_tile;
   size_t fwd_ws, dgrad_ws, wgrad_ws;
   int wg_MO, wg_WNC, wg_splits;
@@ -1927,7 +1930,6 @@ void plan_conv(int dtype, pg_conv_desc* d, int* path, int* tile, size_t* ws) {
   *tile = -1;
   if (dtype == PG_BF16) {
     if (conv_lr_ok(d)) { *path = 2; *ws = 0; return; }
-    if (conv_kg_ok(d)) { *path = 3; *ws = 0; return; }
     if (conv_hr_ok(d)) { *path = 1; *tile = conv_hr_tile(d); *ws = 0; }
   }
 }
@@ -1954,7 +1956,7 @@ int pg_step_plan_create(int dtype, int n_depths, const int* depths, int stage, i
     pg_conv_desc g = d;   // input gradient: the transposed conv, cout -> cin channels
     g.cin = cout; g.cout = (cin + 3) & ~3; g.x_cs = cinp_of(cout); g.y_cs = g.cout; g.flags = 0;
     plan_conv(dtype, &g, &L.dgrad_path, &L.dgrad_tile, &L.dgrad_ws);
-    L.wgrad_ws = dtype == PG_BF16 ? wgrad_bf16_ws_bytes(&d) : 0;
+    L.wgrad_ws = dtype == PG_BF16 ? wgrad_bf16_ws_bytes(&d) : wgrad_f32_ws_bytes(&d);
     if (dtype == PG_BF16) {
       const WgbPlan w = wgrad_bf16_plan(&d);
       L.wg_MO = w.MO; L.wg_WNC = w.WNC; L.wg_splits = w.splits;
@@ -1984,7 +1986,7 @@ size_t pg_step_plan_workspace_size(const pg_step_plan* plan) { return plan ? pla
 
 int pg_step_plan_describe(const pg_step_plan* plan, char* buf, size_t len) {
   PG_CHECK_ARG(plan && buf && len > 0, "step_plan_describe: bad arguments");
-  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr", "conv_kg"};
+  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr"};
   size_t o = 0;
   auto put = [&](const char* fmt, auto... a) {
     if (o < len) o += snprintf(buf + o, len - o, fmt, a...);

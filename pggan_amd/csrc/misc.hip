@@ -242,11 +242,15 @@ __global__ void rgb_dgrad_kernel(int B, int Rx, int C, int x_cs, const float* w,
 }
 
 // dw[o][k] += f * sum_pix g[o][pix] x[pix][k]; db[o] += f * sum_pix g[o][pix]
-// (x at resolution Rx; child=1: g at 2*Rx summed over 2x2 children)
+// (x at resolution Rx; child=1: g at 2*Rx summed over 2x2 children).  Block totals in tot
+// (NA = 3C + 3: dw in [o][k] order, then db), summed over blocks by det_commit.
 template <typename T>
-__global__ void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x, float f, int child,
-                                 const float* gimg, float* dw, float* db, int pix_per_block) {
+__global__ __launch_bounds__(256) void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x,
+                                                        float f, int child, const float* gimg,
+                                                        float* dw, float* db, int pix_per_block,
+                                                        float* scratch) {
   __shared__ float red[256 * 4];
+  __shared__ float tot[2048];   // 3C + 3 <= 1539 totals, then det_commit's tmp
   const int Ri = child ? 2 * Rx : Rx;
   const size_t npix = (size_t)B * Rx * Rx;
   const size_t p0 = (size_t)blockIdx.x * pix_per_block;
@@ -278,21 +282,21 @@ __global__ void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x, flo
         t1 += red[(q * C + threadIdx.x) * 4 + 1];
         t2 += red[(q * C + threadIdx.x) * 4 + 2];
       }
-      atomicAdd(dw + threadIdx.x, f * t0);
-      atomicAdd(dw + C + threadIdx.x, f * t1);
-      atomicAdd(dw + 2 * C + threadIdx.x, f * t2);
+      tot[threadIdx.x] = t0;
+      tot[C + threadIdx.x] = t1;
+      tot[2 * C + threadIdx.x] = t2;
     }
     __syncthreads();
     red[threadIdx.x * 4 + 0] = s0; red[threadIdx.x * 4 + 1] = s1; red[threadIdx.x * 4 + 2] = s2;
     __syncthreads();
-    if (threadIdx.x == 0 && db) {
+    if (threadIdx.x == 0) {
       float t0 = 0.f, t1 = 0.f, t2 = 0.f;
       for (int q = 0; q < ppi; ++q) {
         t0 += red[(q * C) * 4 + 0];
         t1 += red[(q * C) * 4 + 1];
         t2 += red[(q * C) * 4 + 2];
       }
-      atomicAdd(db + 0, f * t0); atomicAdd(db + 1, f * t1); atomicAdd(db + 2, f * t2);
+      tot[3 * C] = t0; tot[3 * C + 1] = t1; tot[3 * C + 2] = t2;
     }
   } else {
     for (int k = threadIdx.x; k < C; k += blockDim.x) {
@@ -303,20 +307,26 @@ __global__ void rgb_wgrad_kernel(int B, int Rx, int C, int x_cs, const T* x, flo
         a0 += g0 * xv; a1 += g1 * xv; a2 += g2 * xv;
         s0 += g0; s1 += g1; s2 += g2;
       }
-      atomicAdd(dw + k, f * a0); atomicAdd(dw + C + k, f * a1); atomicAdd(dw + 2 * C + k, f * a2);
-      if (k == 0 && db) { atomicAdd(db + 0, f * s0); atomicAdd(db + 1, f * s1); atomicAdd(db + 2, f * s2); }
+      tot[k] = a0; tot[C + k] = a1; tot[2 * C + k] = a2;
+      if (k == 0) { tot[3 * C] = s0; tot[3 * C + 1] = s1; tot[3 * C + 2] = s2; }
     }
   }
+  __syncthreads();
+  det_commit(tot, 3 * C + 3, scratch, tot, [&](int q, float t) {
+    float* d = q < 3 * C ? (dw ? dw + q : nullptr) : (db ? db + (q - 3 * C) : nullptr);
+    if (d) *d += f * t;
+  });
 }
 
 // Register-accumulating wgrad of the 1x1 RGB layers for small channel counts (the
 // 512^2 / 1024^2 layers with 16-32 channels are where these bytes are): one pixel per
-// thread per iteration, NA accumulators per thread, butterfly + LDS block reduction,
-// one atomic per accumulator per block.
+// thread per iteration, NA accumulators per thread, butterfly + LDS block reduction into the
+// block's totals, summed over blocks by det_commit.
 // accumulators [0, NW) go to dw[q], [NW, NA) to db[q - NW] (either may be NULL)
 template <int NA, int NW>
-__device__ __forceinline__ void block_reduce_atomic(float (&a)[NA], float* red, float* dw,
-                                                    float* db, float scale) {
+__device__ __forceinline__ void block_reduce_det(float (&a)[NA], float* red, float* dw, float* db,
+                                                 float scale, float* scratch) {
+  __shared__ float det_tmp[NA > 1024 ? NA : 1024];
 #pragma unroll
   for (int q = 0; q < NA; ++q) a[q] = wave_sum(a[q]);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -327,15 +337,19 @@ __device__ __forceinline__ void block_reduce_atomic(float (&a)[NA], float* red, 
   for (int q = threadIdx.x; q < NA; q += blockDim.x) {
     float t = 0.f;
     for (int w = 0; w < nw; ++w) t += red[w * NA + q];
-    float* d = q < NW ? (dw ? dw + q : nullptr) : (db ? db + (q - NW) : nullptr);
-    if (d) atomicAdd(d, t * scale);
+    det_tmp[q] = t;
   }
+  __syncthreads();
+  det_commit(det_tmp, NA, scratch, det_tmp, [&](int q, float t) {
+    float* d = q < NW ? (dw ? dw + q : nullptr) : (db ? db + (q - NW) : nullptr);
+    if (d) *d += t * scale;
+  });
 }
 
 // toRGB wgrad: dw[o][k] += f * sum_pix g[o][pix] x[pix][k], db[o] += f * sum g[o][pix]
 template <typename T, int C>
 __global__ __launch_bounds__(256) void rgb_wgrad_small(int B, int Rx, int x_cs, const T* x, float f, int child,
-                                const float* gimg, float* dw, float* db) {
+                                const float* gimg, float* dw, float* db, float* scratch) {
   __shared__ float red[4 * (3 * C + 3)];
   const int Ri = child ? 2 * Rx : Rx;
   const size_t npix = (size_t)B * Rx * Rx;
@@ -368,7 +382,7 @@ __global__ __launch_bounds__(256) void rgb_wgrad_small(int B, int Rx, int x_cs, 
 #pragma unroll
     for (int o = 0; o < 3; ++o) acc[3 * C + o] += gv[o];
   }
-  block_reduce_atomic<3 * C + 3, 3 * C>(acc, red, dw, db, f);
+  block_reduce_det<3 * C + 3, 3 * C>(acc, red, dw, db, f, scratch);
 }
 
 __device__ __forceinline__ void img_in3(const ImgSrc& img, int bi, int R, int py, int px, int down,
@@ -422,11 +436,13 @@ __global__ void from_rgb_kernel(int B, int R, int C, ImgSrc img, int down, const
 
 // gimg (at the input resolution) += c * sum_o gz[pix_out][o] W[o][i] (* 0.25 if down); ow:
 // gimg = (no accumulation); norms: norms[b] += sum of the final gimg^2 of sample b.  grid =
-// (ceil(Ri / 256), B * Ri): a block is 256 pixels of one image row (one sample)
+// (ceil(Ri / 256), B * Ri): a block is 256 pixels of one image row (one sample); the blocks of
+// a sample are a contiguous index range, so the norms are a segmented det_commit.
 template <typename T>
 __global__ __launch_bounds__(256) void from_rgb_dgrad_kernel(int R, int C, int down, const float* w,
                                                              float c, int gz_cs, const T* gz,
-                                                             float* gimg, int ow, float* norms) {
+                                                             float* gimg, int ow, float* norms,
+                                                             int B, float* scratch) {
   const int Ri = down ? 2 * R : R;
   const float f = down ? 0.25f * c : c;
   const int px = blockIdx.x * 256 + threadIdx.x;
@@ -458,17 +474,21 @@ __global__ __launch_bounds__(256) void from_rgb_dgrad_kernel(int R, int C, int d
   }
   if (norms) {   // uniform
     __shared__ float red[4];
+    __shared__ float tmp[1024];
     const float t = block_sum(q, red);
-    if (threadIdx.x == 0) atomicAdd(norms + bi, t);
+    det_commit_seg(t, B, scratch, tmp, [&](int b, float v) { norms[b] += v; });
   }
 }
 
 // dw[o][i] += c * sum_pix gz[pix][o] img_in[i][pix]; db[o] += c * sum gz[pix][o]
+// (block totals: [o][i] then db, NA = 4C, summed over blocks by det_commit)
 template <typename T>
-__global__ void from_rgb_wgrad_kernel(int B, int R, int C, ImgSrc img, int down, float c,
-                                      int gz_cs, const T* gz, float* dw, float* db,
-                                      int pix_per_block) {
+__global__ __launch_bounds__(256) void from_rgb_wgrad_kernel(int B, int R, int C, ImgSrc img, int down,
+                                                             float c, int gz_cs, const T* gz, float* dw,
+                                                             float* db, int pix_per_block,
+                                                             float* scratch) {
   __shared__ float red[256 * 4];
+  __shared__ float tot[2048];   // 4C <= 2048 totals, then det_commit's tmp
   const size_t npix = (size_t)B * R * R;
   const size_t p0 = (size_t)blockIdx.x * pix_per_block;
   const size_t p1 = p0 + pix_per_block < npix ? p0 + pix_per_block : npix;
@@ -493,31 +513,30 @@ __global__ void from_rgb_wgrad_kernel(int B, int R, int C, ImgSrc img, int down,
       for (int q = 0; q < ppi; ++q)
 #pragma unroll
         for (int j = 0; j < 4; ++j) t[j] += red[(q * C + threadIdx.x) * 4 + j];
-      if (dw) {
-        atomicAdd(dw + threadIdx.x * 3 + 0, c * t[0]);
-        atomicAdd(dw + threadIdx.x * 3 + 1, c * t[1]);
-        atomicAdd(dw + threadIdx.x * 3 + 2, c * t[2]);
-      }
-      if (db) atomicAdd(db + threadIdx.x, c * t[3]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) tot[threadIdx.x * 3 + j] = t[j];
+      tot[3 * C + threadIdx.x] = t[3];
     }
   } else {
     for (int o = threadIdx.x; o < C; o += blockDim.x) {
       float a[4] = {0.f, 0.f, 0.f, 0.f};
       accum(o, p0, p1, 1, a);
-      if (dw) {
-        atomicAdd(dw + o * 3 + 0, c * a[0]);
-        atomicAdd(dw + o * 3 + 1, c * a[1]);
-        atomicAdd(dw + o * 3 + 2, c * a[2]);
-      }
-      if (db) atomicAdd(db + o, c * a[3]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) tot[o * 3 + j] = a[j];
+      tot[3 * C + o] = a[3];
     }
   }
+  __syncthreads();
+  det_commit(tot, 4 * C, scratch, tot, [&](int q, float t) {
+    float* d = q < 3 * C ? (dw ? dw + q : nullptr) : (db ? db + (q - 3 * C) : nullptr);
+    if (d) *d += c * t;
+  });
 }
 
 // fromRGB wgrad for small C: dw[o][i] += c sum gz[pix][o] img_in[i][pix], db[o] += c sum gz
 template <typename T, int C>
 __global__ __launch_bounds__(256) void from_rgb_wgrad_small(int B, int R, ImgSrc img, int down, float c,
-                                     int gz_cs, const T* gz, float* dw, float* db) {
+                                     int gz_cs, const T* gz, float* dw, float* db, float* scratch) {
   __shared__ float red[4 * 4 * C];
   const size_t npix = (size_t)B * R * R;
   float acc[4 * C];
@@ -541,7 +560,7 @@ __global__ __launch_bounds__(256) void from_rgb_wgrad_small(int B, int R, ImgSrc
       }
     }
   }
-  block_reduce_atomic<4 * C, 3 * C>(acc, red, dw, db, c);
+  block_reduce_det<4 * C, 3 * C>(acc, red, dw, db, c, scratch);
 }
 
 __global__ void img_fade_kernel(int B, int C, int R, const float* x, float alpha, float* out) {
@@ -1014,8 +1033,10 @@ __global__ void drift_kernel(int B, const float* l, float w, float* loss, float*
   if (threadIdx.x == 0 && loss) loss[0] += w * t;
 }
 
-__global__ void r1_kernel(int B, size_t n, const float* g, float* r1, float* gbar) {
+__global__ __launch_bounds__(256) void r1_kernel(int B, size_t n, const float* g, float* r1,
+                                                  float* gbar, float* scratch) {
   __shared__ float red[16];
+  __shared__ float tmp[1024];
   float part = 0.f;
   const float inv = 1.f / (float)B;
   if ((n & 3) == 0 && (((uintptr_t)g | (uintptr_t)gbar) & 15) == 0) {
@@ -1046,7 +1067,7 @@ __global__ void r1_kernel(int B, size_t n, const float* g, float* r1, float* gba
     }
   }
   const float t = block_sum(part, red);
-  if (threadIdx.x == 0) atomicAdd(r1, 0.5f * t * inv);
+  det_commit_seg(t, 1, scratch, tmp, [&](int, float v) { r1[0] += 0.5f * v * inv; });
 }
 
 __global__ void gp_interp_kernel(int B, size_t per, const float* xr, const float* xf,
@@ -1058,8 +1079,11 @@ __global__ void gp_interp_kernel(int B, size_t per, const float* xr, const float
   }
 }
 
-__global__ void sumsq_per_sample_kernel(int B, size_t per, const float* g, float* norms) {
+// grid (gx, B): the blocks of sample b are the contiguous index range [b gx, (b + 1) gx)
+__global__ __launch_bounds__(256) void sumsq_per_sample_kernel(int B, size_t per, const float* g,
+                                                               float* norms, float* scratch) {
   __shared__ float red[16];
+  __shared__ float tmp[1024];
   const int b = blockIdx.y;
   float part = 0.f;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < per;
@@ -1068,7 +1092,7 @@ __global__ void sumsq_per_sample_kernel(int B, size_t per, const float* g, float
     part += v * v;
   }
   const float t = block_sum(part, red);
-  if (threadIdx.x == 0) atomicAdd(norms + b, t);
+  det_commit_seg(t, B, scratch, tmp, [&](int q, float v) { norms[q] += v; });
 }
 
 __global__ void gp_finish_kernel(int B, size_t per, const float* g, float w, const float* sumsq,
@@ -1382,14 +1406,30 @@ int pg_rgb_out(int dtype, int B, int R, int C, int x_cs, const void* x, const fl
 
 }  // extern "C"
 
+// pixel blocks of the generic RGB weight-gradient kernels: ~1024 pixels per block, at most 4096
+// blocks, and at most as many as the det_commit scratch holds with na totals per block
+static void rgb_wgrad_blocks(size_t npix, int na, int* blocks_out, int* ppb_out) {
+  int cap = (int)(pg_scratch_floats() / (size_t)na);
+  if (cap > 4096) cap = 4096;
+  int ppb = 1024;
+  int blocks = (int)((npix + ppb - 1) / ppb);
+  if (blocks > cap) {
+    blocks = cap;
+    ppb = (int)((npix + blocks - 1) / blocks);
+    blocks = (int)((npix + ppb - 1) / ppb);
+  }
+  *blocks_out = blocks;
+  *ppb_out = ppb;
+}
+
 template <typename T>
 static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* w, float c, int Cp,
                         int xp_cs, const T* xp, const float* wp, float cp, float alpha,
                         const float* gimg, T* gx, T* gxp, float* dw, float* db, float* dwp,
-                        float* dbp, hipStream_t st) {
+                        float* dbp, float* scratch, hipStream_t st) {
   const float fa = xp ? alpha * c : c;
   size_t n = (size_t)B * R * R * (C / 4);
-  if (rgb_bwd_part<T>(B, R, C, x_cs, x, w, fa, 0, gimg, gx, dw, db, st) == 0) {
+  if (rgb_bwd_part<T>(B, R, C, x_cs, x, w, fa, 0, gimg, gx, dw, db, scratch, st) == 0) {
     gx = nullptr;
     dw = nullptr;
   }
@@ -1398,27 +1438,26 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
                        fa, 0, gimg, gx);
   {
     const size_t npix = (size_t)B * R * R;
-    int ppb = 1024;
-    int blocks = (int)((npix + ppb - 1) / ppb);
-    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    int ppb, blocks;
+    rgb_wgrad_blocks(npix, 3 * C + 3, &blocks, &ppb);
     if (dw) {
       const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       if (C == 16)
         PG_KLAUNCH((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
-                           gimg, dw, db);
+                           gimg, dw, db, scratch);
       else if (C == 32)
         PG_KLAUNCH((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, R, x_cs, x, fa, 0,
-                           gimg, dw, db);
+                           gimg, dw, db, scratch);
       else
         PG_KLAUNCH(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, R, C, x_cs, x, fa,
-                           0, gimg, dw, db, ppb);
+                           0, gimg, dw, db, ppb, scratch);
     }
   }
   if (xp) {
     const int Rp = R / 2;
     const float fp = (1.f - alpha) * cp;
     n = (size_t)B * Rp * Rp * (Cp / 4);
-    if (rgb_bwd_part<T>(B, Rp, Cp, xp_cs, xp, wp, fp, 1, gimg, gxp, dwp, dbp, st) == 0) {
+    if (rgb_bwd_part<T>(B, Rp, Cp, xp_cs, xp, wp, fp, 1, gimg, gxp, dwp, dbp, scratch, st) == 0) {
       gxp = nullptr;
       dwp = nullptr;
     }
@@ -1426,20 +1465,19 @@ static int rgb_bwd_impl(int B, int R, int C, int x_cs, const T* x, const float* 
       PG_KLAUNCH(rgb_dgrad_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, B, Rp, Cp, xp_cs,
                          wp, fp, 1, gimg, gxp);
     const size_t npix = (size_t)B * Rp * Rp;
-    int ppb = 1024;
-    int blocks = (int)((npix + ppb - 1) / ppb);
-    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    int ppb, blocks;
+    rgb_wgrad_blocks(npix, 3 * Cp + 3, &blocks, &ppb);
     if (dwp) {
       const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
       if (Cp == 16)
         PG_KLAUNCH((rgb_wgrad_small<T, 16>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
-                           1, gimg, dwp, dbp);
+                           1, gimg, dwp, dbp, scratch);
       else if (Cp == 32)
         PG_KLAUNCH((rgb_wgrad_small<T, 32>), dim3(gb), dim3(256), 0, st, B, Rp, xp_cs, xp, fp,
-                           1, gimg, dwp, dbp);
+                           1, gimg, dwp, dbp, scratch);
       else
         PG_KLAUNCH(rgb_wgrad_kernel<T>, dim3(blocks), dim3(256), 0, st, B, Rp, Cp, xp_cs, xp,
-                           fp, 1, gimg, dwp, dbp, ppb);
+                           fp, 1, gimg, dwp, dbp, ppb, scratch);
     }
   }
   PG_LAUNCH_CHECK();
@@ -1451,14 +1489,16 @@ extern "C" {
 int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, const float* w,
                    float c, int Cp, int xp_cs, const void* xp, const float* wp, float cp,
                    float alpha, const float* gimg, void* gx, void* gxp, float* dw, float* db,
-                   float* dwp, float* dbp, void* stream) {
+                   float* dwp, float* dbp, void* scratch, void* stream) {
   PG_CHECK_ARG(x && w && gimg && C % 4 == 0 && (!xp || (wp && Cp % 4 == 0)), "rgb_out_bwd: bad args");
+  PG_CHECK_ARG(scratch || !(dw || db || dwp || dbp), "rgb_out_bwd: weight gradients need scratch");
   hipStream_t st = (hipStream_t)stream;
+  float* sc = (float*)scratch;
   if (dtype == PG_F32)
     return rgb_bwd_impl<float>(B, R, C, x_cs, (const float*)x, w, c, Cp, xp_cs, (const float*)xp,
-                               wp, cp, alpha, gimg, (float*)gx, (float*)gxp, dw, db, dwp, dbp, st);
+                               wp, cp, alpha, gimg, (float*)gx, (float*)gxp, dw, db, dwp, dbp, sc, st);
   return rgb_bwd_impl<bf16_t>(B, R, C, x_cs, (const bf16_t*)x, w, c, Cp, xp_cs, (const bf16_t*)xp,
-                              wp, cp, alpha, gimg, (bf16_t*)gx, (bf16_t*)gxp, dw, db, dwp, dbp, st);
+                              wp, cp, alpha, gimg, (bf16_t*)gx, (bf16_t*)gxp, dw, db, dwp, dbp, sc, st);
 }
 
 int pg_rgb_out_bwd_pn(int dtype, int B, int R, int C, int y_cs, const void* y, const float* r,
@@ -1531,53 +1571,56 @@ int pg_from_rgb_bits(int dtype, int B, int R, int C, const pg_img_src* img, int 
 
 static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, int down,
                              const float* w, float c, int gz_cs, const void* gz, float* gimg, int ow,
-                             float* norms, float* dw, float* db, hipStream_t st) {
+                             float* norms, float* dw, float* db, float* scratch, hipStream_t st) {
   PG_CHECK_ARG(w && gz && C % 4 == 0, "from_rgb_bwd: bad args");
   PG_CHECK_ARG(!(dw || db) || img, "from_rgb_bwd: wgrad needs img");
   PG_CHECK_ARG(!norms || gimg, "from_rgb_bwd: norms need gimg");
+  PG_CHECK_ARG(scratch || !(dw || db || norms), "from_rgb_bwd: weight gradients / norms need scratch");
   if ((dtype == PG_F32 ? try_from_rgb_bwd<float>(B, R, C, img, down, w, c, gz_cs, (const float*)gz,
-                                                 gimg, ow, norms, dw, db, st)
+                                                 gimg, ow, norms, dw, db, scratch, st)
                        : try_from_rgb_bwd<bf16_t>(B, R, C, img, down, w, c, gz_cs,
-                                                  (const bf16_t*)gz, gimg, ow, norms, dw, db, st)) == 0) {
+                                                  (const bf16_t*)gz, gimg, ow, norms, dw, db, scratch,
+                                                  st)) == 0) {
     PG_LAUNCH_CHECK();
     return PG_OK;
   }
   if (gimg) {
     const int Ri = down ? 2 * R : R;
     const dim3 grid((Ri + 255) / 256, B * Ri);
+    PG_CHECK_ARG(!norms || pg_det_fits((size_t)grid.x * grid.y, 1), "from_rgb_bwd: too many rows");
     if (dtype == PG_F32)
       PG_KLAUNCH(from_rgb_dgrad_kernel<float>, grid, dim3(256), 0, st, R, C, down, w, c,
-                         gz_cs, (const float*)gz, gimg, ow, norms);
+                         gz_cs, (const float*)gz, gimg, ow, norms, B, scratch);
     else
       PG_KLAUNCH(from_rgb_dgrad_kernel<bf16_t>, grid, dim3(256), 0, st, R, C, down, w, c,
-                         gz_cs, (const bf16_t*)gz, gimg, ow, norms);
+                         gz_cs, (const bf16_t*)gz, gimg, ow, norms, B, scratch);
   }
   if (dw || db) {
     const size_t npix = (size_t)B * R * R;
-    int ppb = 1024;
-    int blocks = (int)((npix + ppb - 1) / ppb);
-    if (blocks > 4096) { blocks = 4096; ppb = (int)((npix + blocks - 1) / blocks); blocks = (int)((npix + ppb - 1) / ppb); }
+    int ppb, blocks;
+    PG_CHECK_ARG(C <= 512, "from_rgb_bwd: C %d > 512", C);
+    rgb_wgrad_blocks(npix, 4 * C, &blocks, &ppb);
     const int gb = (int)((npix + 255) / 256 < 1024 ? (npix + 255) / 256 : 1024);
     if (dtype == PG_F32) {
       if (C == 16)
         PG_KLAUNCH((from_rgb_wgrad_small<float, 16>), dim3(gb), dim3(256), 0, st, B, R, img,
-                           down, c, gz_cs, (const float*)gz, dw, db);
+                           down, c, gz_cs, (const float*)gz, dw, db, scratch);
       else if (C == 32)
         PG_KLAUNCH((from_rgb_wgrad_small<float, 32>), dim3(gb), dim3(256), 0, st, B, R, img,
-                           down, c, gz_cs, (const float*)gz, dw, db);
+                           down, c, gz_cs, (const float*)gz, dw, db, scratch);
       else
         PG_KLAUNCH(from_rgb_wgrad_kernel<float>, dim3(blocks), dim3(256), 0, st, B, R, C,
-                           img, down, c, gz_cs, (const float*)gz, dw, db, ppb);
+                           img, down, c, gz_cs, (const float*)gz, dw, db, ppb, scratch);
     } else {
       if (C == 16)
         PG_KLAUNCH((from_rgb_wgrad_small<bf16_t, 16>), dim3(gb), dim3(256), 0, st, B, R,
-                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db, scratch);
       else if (C == 32)
         PG_KLAUNCH((from_rgb_wgrad_small<bf16_t, 32>), dim3(gb), dim3(256), 0, st, B, R,
-                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db);
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db, scratch);
       else
         PG_KLAUNCH(from_rgb_wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, R, C,
-                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb);
+                           img, down, c, gz_cs, (const bf16_t*)gz, dw, db, ppb, scratch);
     }
   }
   PG_LAUNCH_CHECK();
@@ -1586,17 +1629,18 @@ static int from_rgb_bwd_impl(int dtype, int B, int R, int C, const ImgSrc& img, 
 
 int pg_from_rgb_bwd(int dtype, int B, int R, int C, const float* img, int down, const float* w,
                     float c, int gz_cs, const void* gz, float* gimg, float* dw, float* db,
-                    void* stream) {
+                    void* scratch, void* stream) {
   return from_rgb_bwd_impl(dtype, B, R, C, ImgSrc(img), down, w, c, gz_cs, gz, gimg, 0, nullptr,
-                           dw, db, (hipStream_t)stream);
+                           dw, db, (float*)scratch, (hipStream_t)stream);
 }
 
 int pg_from_rgb_bwd_src(int dtype, int B, int R, int C, const pg_img_src* img, int down,
                         const float* w, float c, int gz_cs, const void* gz, float* gimg,
-                        int gimg_overwrite, float* norms, float* dw, float* db, void* stream) {
+                        int gimg_overwrite, float* norms, float* dw, float* db, void* scratch,
+                        void* stream) {
   PG_CHECK_ARG(!img || !img->x1 || (img->a && img->c), "from_rgb_bwd_src: bad image source");
   return from_rgb_bwd_impl(dtype, B, R, C, img ? ImgSrc(*img) : ImgSrc(), down, w, c, gz_cs, gz,
-                           gimg, gimg_overwrite, norms, dw, db, (hipStream_t)stream);
+                           gimg, gimg_overwrite, norms, dw, db, (float*)scratch, (hipStream_t)stream);
 }
 
 int pg_penalty_scale(int mode, int B, float* norms, float w, float* loss_out, float* scale,
@@ -1779,10 +1823,13 @@ int pg_drift_loss(int B, const float* logits, float w, float* loss_out, float* u
   return PG_OK;
 }
 
-int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* stream) {
-  PG_CHECK_ARG(g && r1_out && B > 0, "r1_penalty: bad args");
+size_t pg_scratch_bytes(void) { return PG_SCRATCH_BYTES; }
+
+int pg_r1_penalty(int B, size_t n, const float* g, float* r1_out, float* gbar, void* scratch,
+                  void* stream) {
+  PG_CHECK_ARG(g && r1_out && B > 0 && scratch, "r1_penalty: bad args (scratch required)");
   PG_KLAUNCH(r1_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0, (hipStream_t)stream, B,
-                     n, g, r1_out, gbar);
+                     n, g, r1_out, gbar, (float*)scratch);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1797,12 +1844,14 @@ int pg_gp_interp(int B, size_t per, const float* xr, const float* xf, const floa
 }
 
 int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, float* norms,
-                  float* gbar, void* stream) {
-  PG_CHECK_ARG(g && gp_out && norms && gbar, "gp_penalty: bad args");
+                  float* gbar, void* scratch, void* stream) {
+  PG_CHECK_ARG(g && gp_out && norms && gbar && scratch, "gp_penalty: bad args (scratch required)");
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(norms, 0, sizeof(float) * B, st);
   int gx = grid_for(per, 256, 256);
-  PG_KLAUNCH(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms);
+  PG_CHECK_ARG(pg_det_fits((size_t)gx * B, 1), "gp_penalty: B too large for the scratch");
+  PG_KLAUNCH(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms,
+                     (float*)scratch);
   PG_KLAUNCH(gp_finish_kernel, dim3(grid_for((size_t)B * per)), dim3(256), 0, st, B, per, g,
                      w, norms, gp_out, gbar);
   PG_LAUNCH_CHECK();
@@ -1869,19 +1918,6 @@ static int pg_hip_status(hipError_t e, const char* what) {
   return PG_ERR_HIP;
 }
 
-}  // extern "C"
-// the event armed for the next launch on one stream (per host thread)
-static thread_local hipEvent_t g_arm_ev = nullptr;
-static thread_local hipStream_t g_arm_st = nullptr;
-
-hipEvent_t pg_take_armed_event(hipStream_t s) {
-  if (!g_arm_ev || s != g_arm_st) return nullptr;
-  hipEvent_t e = g_arm_ev;
-  g_arm_ev = nullptr;
-  return e;
-}
-extern "C" {
-
 int pg_stream_create(int lowest_priority, void** stream) {
   PG_CHECK_ARG(stream, "stream_create: null out");
   int least = 0, greatest = 0;
@@ -1899,14 +1935,6 @@ int pg_stream_destroy(void* stream) {
   if (!stream) return PG_OK;
   return pg_hip_status(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
 }
-
-int pg_event_arm(void* ev, void* stream) {
-  g_arm_ev = (hipEvent_t)ev;
-  g_arm_st = (hipStream_t)stream;
-  return PG_OK;
-}
-
-int pg_event_armed(void) { return g_arm_ev != nullptr; }
 
 int pg_event_create(int timing, void** ev) {
   PG_CHECK_ARG(ev, "event_create: null out");

@@ -170,13 +170,50 @@ class Hyper:
 # inline on the current stream so per-launch HIP event durations exclude overlap
 FORCE_SERIAL = False
 
+# Schedule options: attributes of StepEngine, set by keyword (tests) or, for A/B runs, by ONE
+# environment string PG_ENGINE="name=value,..." (tools/ab.sh).  Every default is the measured
+# faster choice (DESIGN.md performance log); the alternatives stay because the engine needs them
+# anyway (batch sizes that are not a multiple of 4, the bucketed DP exchange, the fp32 parity
+# mode, the CPU test double).
+ENGINE_DEFAULTS = dict(
+    merge_d=True,          # the D half's real / fake forward and second backward at batch 2B
+    merge_g=True,          # both generator forwards of a step at batch 2B
+    side_stream=True,      # weight gradients on a least-priority side stream
+    elide_zero_blend=True,  # alpha = 1: skip the exactly-zero fade-in branches
+    fuse_pixnorm=True,     # PixelNorm in the G conv epilogues
+    fuse_pnbwd=True,       # G PixelNorm backward in the input-gradient conv epilogue
+    fuse_pn_pool=True,     # ... also after the pool of the next level's conv-a input gradient
+    fuse_rgb_pnbwd=True,   # the toRGB input gradient with the top PixelNorm backward
+    fuse_dbits=True,       # D conv+lrelu+pool outputs as sign bits (see _dbits)
+    dbits_min_res=512,     # ... from this resolution; below it the unpool-pass bits (_ubits)
+    fuse_ubits=True,
+    fuse_rgbbits=True,     # the top fromRGB output's sign bits (see _rgbbits)
+)
+
+
+def engine_options(overrides=None):
+    """ENGINE_DEFAULTS with the PG_ENGINE environment string and then `overrides` applied."""
+    opts = dict(ENGINE_DEFAULTS)
+    for item in filter(None, os.environ.get("PG_ENGINE", "").split(",")):
+        k, _, v = item.partition("=")
+        k = k.strip()
+        if k not in opts:
+            raise ValueError(f"PG_ENGINE: unknown option {k!r} (known: {sorted(opts)})")
+        opts[k] = type(opts[k])(int(v)) if isinstance(opts[k], (bool, int)) else type(opts[k])(v)
+    for k, v in (overrides or {}).items():
+        if k not in opts:
+            raise ValueError(f"unknown engine option {k!r}")
+        opts[k] = v
+    return opts
+
 
 class StepEngine:
     """All device buffers and kernel schedules for one (stage, batch, dtype)."""
 
-    def __init__(self, ops, depths, s, B, device, latent_dim=512, forward_only=None):
+    def __init__(self, ops, depths, s, B, device, latent_dim=512, forward_only=None, **options):
         """forward_only: "G" or "D" allocates just that net's forward activations (the
-        inference / sampling path of nets.Generator / nets.Discriminator.forward)."""
+        inference / sampling path of nets.Generator / nets.Discriminator.forward).
+        options: schedule options (ENGINE_DEFAULTS)."""
         self.ops, self.depths, self.s, self.B = ops, list(depths), s, B
         self.forward_only = forward_only
         self.dev = device
@@ -187,12 +224,8 @@ class StepEngine:
         self.d0 = d[0]
         self.mcs = cinp(d[0] + 1)
         self.keep_fake_D = False
-        self.fuse_pixnorm = True   # PixelNorm in the G conv epilogues where the kernel allows
-        self.fuse_dbits = True     # D conv+lrelu+pool outputs kept as sign bits (see _dbits)
-        # tuning runs only: PG_DBITS_MIN_RES (sign-bit D activations from this resolution)
-        self.dbits_min_res = int(os.environ.get("PG_DBITS_MIN_RES", "512"))
-        # tuning / A-B runs only: PG_PNBWD=0 keeps the G PixelNorm backward as its own pass
-        self.fuse_pnbwd = os.environ.get("PG_PNBWD", "1") != "0"
+        for k, v in engine_options(options).items():
+            setattr(self, k, v)
         self.ws = None          # split-K workspace (fp32), grown on first use
         self._ws_cache = {}
         self.plan = None        # pg_step_plan description (HIP library)
@@ -202,12 +235,11 @@ class StepEngine:
             need, self.plan = ops.step_plan(self.depths, s, B)
             if need:
                 self.ws = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
-        # alpha == 1: the low-resolution branches of the fade-in (toRGB / fromRGB of the
-        # previous level, the real-image fade) are multiplied by exactly 0 in the reference
-        # (pggan/nets.py:155-156,263-265, pggan/model.py:217-221) and contribute exactly 0 to
-        # every output and gradient; elide them (bit-identical).  Their
-        # parameters still get a zero gradient and the Adam step, as in the reference.
-        self.elide_zero_blend = os.environ.get("PG_ELIDE_BLEND", "1") != "0"
+        # alpha == 1 (elide_zero_blend): the low-resolution branches of the fade-in (toRGB /
+        # fromRGB of the previous level, the real-image fade) are multiplied by exactly 0 in the
+        # reference (pggan/nets.py:155-156,263-265, pggan/model.py:217-221) and contribute exactly
+        # 0 to every output and gradient; elide them.  Their parameters
+        # still get a zero gradient and the Adam step, as in the reference.
         self._last_dlow = True
         # trace(net, engine) after every G / D forward, or None: parity tests read the
         # leaky-ReLU region choices of each forward from the activation buffers
@@ -219,70 +251,40 @@ class StepEngine:
         # of a backward pass is off the pass's critical path (the input-gradient chain), so it
         # runs beside the next levels' convs -- at 4^2-32^2 neither launch fills the 256 CUs.
         # One side stream serialises the wgrads among themselves, so every dW accumulates in
-        # the same order as on one stream (bitwise-equal results).  _join() orders the side
-        # stream back into the main one before anything overwrites a wgrad input or reads a
-        # gradient (see _side_join).  PG_SIDE_WGRAD=0 keeps one stream (A/B runs).
+        # the same order as on one stream.  _side_join() orders the side stream back into the
+        # main one before anything overwrites a wgrad input or reads a gradient.  The stream is
+        # the library's least-priority stream (pg_stream_create, one per device and process):
+        # its own hardware-queue pool, so it never shares the main stream's queue (with a torch
+        # pool stream the two landed on one queue in DP runs and serialised: 301 vs 351 img/s,
+        # profiles/r4_side_queue_ab.txt).
         self.side = None
         self._side_ev = {}      # buffer-set key -> last side-stream event reading it
-        self._side_pending = []  # queued side launches (side_batch > 1, see _side_call)
-        self._armed_ev = None    # the event the next main-stream launch records (armed form)
-        self.side_batch = max(1, int(os.environ.get("PG_SIDE_BATCH", "1")))
         self.ws_side = None
-        self._dkey = "D"        # key of the D buffer set in use ("Df": the fake-image pass)
-        if (forward_only is None and str(device).startswith("cuda") and
-                os.environ.get("PG_SIDE_WGRAD", "1") != "0"):
-            # the side stream at the device's least priority, created by the library: its own
-            # hardware-queue pool, so it never shares the main stream's queue.  With 16 queues
-            # per process (DP runs) a torch pool stream landed on the main stream's queue and
-            # serialised the two (DP bookkeeping at one rank: 301 vs 351 img/s; with this
-            # stream 339.5; without DP 351.0 vs 350.3, profiles/r4_side_queue_ab.txt).
-            # PG_SIDE_LOWPRI=0: a torch pool stream (A/B runs).
-            if os.environ.get("PG_SIDE_LOWPRI", "1") != "0" and hasattr(ops, "stream"):
-                self.side = ops.stream(lowest_priority=True)
-            else:
-                self.side = torch.cuda.Stream(device=device)
-        # the fake-image pass of the D half (G forward, D forward + backward) depends on the
-        # real-image part (F, B1, R1, T, B2) only through the parameters, so it runs on its
-        # own stream beside it, with its own D buffer set, split-K workspace, weight-gradient
-        # stream and gradient buffer (summed into D's before Adam_D): the low-resolution
-        # launches of one pass (latency bound, a fraction of the CUs) share the GPU with the
-        # other pass's high-resolution ones.  Measured slower (A/B at C5: 311.0 -> 306.8 img/s,
-        # the two passes' high-resolution launches contend for HBM and the host enqueue grows
-        # 1.5 ms), so it is opt-in: PG_FAKE_STREAM=1.
-        self.fstream = self.side2 = None
-        self.ws_side2 = None
-        if self.side is not None and os.environ.get("PG_FAKE_STREAM", "0") == "1":
-            self.fstream = torch.cuda.Stream(device=device)
-            self.side2 = torch.cuda.Stream(device=device)
-        # PG_MAIN_PRIORITY=1 (A/B runs): the step's main stream (the input-gradient chain, the
-        # critical path) is a high-priority stream, so the dispatcher serves its workgroups
-        # before the side stream's weight gradients when both have work queued
-        self.main_hp = None
-        if self.side is not None and os.environ.get("PG_MAIN_PRIORITY", "0") == "1":
-            self.main_hp = torch.cuda.Stream(device=device,
-                                             priority=torch.cuda.Stream.priority_range()[1])
-        # the cross-stream events: the library's device-scope-release events (pg_event_create)
-        # from a ring.  torch's events release to system scope -- each record writes back and
-        # invalidates every XCD's L2 and delays the stream's next kernel by ~6.5 us, and the step
-        # records ~75 of them.  A ring slot is re-recorded only after 512 more records; a wait
-        # always binds the record made before it, and a join that meets a re-recorded slot waits
-        # for a later point of the side stream (more ordering, never less).
-        # PG_TORCH_EVENTS=1: torch.cuda.Event (A/B runs).
-        self._ev_ring, self._ev_i = None, 0
-        if (self.side is not None and hasattr(ops, "event") and
-                os.environ.get("PG_TORCH_EVENTS", "0") != "1"):
-            self._ev_ring = [ops.event() for _ in range(512)]
-        # PG_ARM_EVENTS=1: the side stream's waits on the main stream use events recorded by
-        # the main kernels themselves (see _side_call)
-        self._arm_events = (self._ev_ring is not None and
-                            os.environ.get("PG_ARM_EVENTS", "0") == "1")
+        if (forward_only is None and str(device).startswith("cuda") and self.side_stream and
+                hasattr(ops, "side_stream")):
+            self.side = ops.side_stream()
+        # the cross-stream events: the library's device-scope-release events (pg_event_create).
+        # torch's events release to system scope (each record writes back and invalidates every
+        # XCD's L2).  Two rings: records on the side stream (the joins wait on those) and records
+        # on the main stream (the side stream's waits): a slot is re-recorded only on its own
+        # stream after 256 more records there, so a join that meets a re-recorded slot waits for
+        # a later point of the same stream -- more ordering, never less.
+        self._ev_side = self._ev_main = None
+        self._ev_si = self._ev_mi = 0
+        if self.side is not None and hasattr(ops, "event"):
+            self._ev_side = [ops.event() for _ in range(256)]
+            self._ev_main = [ops.event() for _ in range(256)]
         self._alloc()
 
-    def _event(self):
-        if self._ev_ring is None:
+    def _event(self, side):
+        """The next event of the side-stream ring (side) or of the main-stream ring."""
+        ring = self._ev_side if side else self._ev_main
+        if ring is None:
             return None
-        ev = self._ev_ring[self._ev_i]
-        self._ev_i = (self._ev_i + 1) % len(self._ev_ring)
+        if side:
+            ev, self._ev_si = ring[self._ev_si], (self._ev_si + 1) % len(ring)
+        else:
+            ev, self._ev_mi = ring[self._ev_mi], (self._ev_mi + 1) % len(ring)
         return ev
 
     # ------------------------------------------------------------------ buffers
@@ -297,13 +299,13 @@ class StepEngine:
         # "Dtrain" (that net's forward + first-order backward: the autograd modules)
         need_G, need_D = fo in (None, "G", "Gtrain"), fo in (None, "D", "Dtrain")
         train = fo in (None, "Gtrain", "Dtrain")
-        merge_d = fo is None and B % 4 == 0 and os.environ.get("PG_MERGE_D", "1") != "0"
+        merge_d = fo is None and B % 4 == 0 and self.merge_d
         # the D half's generator forward (the fake image) and the G half's use the same G
         # parameters (Adam_G runs after the G half): with merge_g they run as ONE forward at
         # batch 2B ([fake for D; fake for G], see _d_step_merged); the G buffers are
         # allocated at 2B, self.g holds first-half views and g_hi the G half's.
-        # PG_MERGE_G=0: separate forwards (A/B runs).  +1.5 % at C5 (profiles/r4_merge_g_ab.txt).
-        merge_g = merge_d and os.environ.get("PG_MERGE_G", "1") != "0"
+        # +1.5 % at C5 (profiles/r4_merge_g_ab.txt).
+        merge_g = merge_d and self.merge_g
         GB = 2 * B if merge_g else B
         self._GBs = (B, 2 * B) if merge_g else (B,)
         self._g_done = False
@@ -348,7 +350,6 @@ class StepEngine:
         # batch), self.dd holds first-half views (every batch-B pass: B1, the tangent, the G
         # half) and the generator's image is the second half of the merged input.  Needs
         # B % 4 == 0 so the minibatch-stddev groups (4 contiguous samples) stay within a half.
-        # PG_MERGE_D=0: separate passes (A/B runs).
         self.dd2 = None
         self._Bs = (B,)
         if merge_d:
@@ -366,10 +367,6 @@ class StepEngine:
                 self.g_hi["img"] = x3[2 * B:]
         else:
             self.dd = self._alloc_D(need_D, train)
-        # the fake-image pass's buffer set (concurrent mode) and its split-K workspace
-        self.dd_f = self._alloc_D(need_D, train) if self.fstream is not None else None
-        self.ws_f = torch.empty_like(self.ws) if (self.fstream is not None and self.ws is not None) \
-            else None
         # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
         self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
 
@@ -392,10 +389,6 @@ class StepEngine:
                 D[f"mb{i}"] = torch.zeros(B, Ri, Ri, (d[i] + 7) // 8, dtype=torch.uint8,
                                           device=self.dev)
                 D[f"a{i}"] = t(B, Ri, Ri, d[i + 1])
-                # lrelu sign bits of the conv-a output (the lrelu' operand of its consumers'
-                # masks where the kernels support it, see _abits)
-                D[f"ab{i}"] = torch.zeros(B, Ri, Ri, (d[i + 1] + 7) // 8, dtype=torch.uint8,
-                                          device=self.dev)
                 D[f"bf{i}"] = t(B, Ri, Ri, d[i])
                 D[f"p{i}"] = t(B, Ri // 2, Ri // 2, d[i])
             D["m"] = t(B, 4, 4, self.mcs)
@@ -551,7 +544,6 @@ class StepEngine:
         need = self._ws_bytes("w", H, cin, cout, ups)
         if need and (self.ws_side is None or self.ws_side.numel() * 4 < need):
             # the side stream may still read the old workspace
-            self._side_flush()
             self.side.synchronize()
             self.ws_side = torch.empty((need + 3) // 4, dtype=torch.float32, device=self.dev)
         self._side_call((net,), self.ops.conv_wgrad, x, gz, dW, B=self.B, H=H, W=H, cin=cin,
@@ -561,51 +553,20 @@ class StepEngine:
     def _side_call(self, nets, fn, *a, **kw):
         """Run a weight-gradient launch `fn` on the side stream (or inline without one).
         nets: whose buffers it reads (joins before those are overwritten).  Its inputs were
-        written on the main stream, so the side stream first waits for it.  With
-        side_batch > 1 the launches are queued on the host and enqueued side_batch at a time
-        behind ONE main-stream event (each event record costs the main stream's next kernel
-        ~6.5 us); _side_flush() also runs at every join, before a grad_ready callback and
-        before the side workspace is replaced."""
+        written on the main stream, so the side stream first waits for it."""
         if self.side is None or FORCE_SERIAL:
             return fn(*a, **kw)
-        if self._arm_events and not torch.cuda.is_current_stream_capturing():
-            # armed form: this launch waits for an event the NEXT main-stream kernel of the
-            # library records at its completion (pg_event_arm: no marker packet in the main
-            # queue); it is enqueued at the next side call or flush, one main kernel later
-            self._side_flush()
-            self._side_pending.append((nets, fn, a, kw))
-            ev = self._event()
-            ev.arm(torch.cuda.current_stream())
-            self._armed_ev = ev
-            return
-        self._side_pending.append((nets, fn, a, kw))
-        if len(self._side_pending) >= self.side_batch:
-            self._side_flush()
-
-    def _side_flush(self):
-        if not self._side_pending:
-            return
-        pend, self._side_pending = self._side_pending, []
-        ev, self._armed_ev = self._armed_ev, None
-        if ev is not None:
-            if self.ops.lib.pg_event_armed():   # no library launch on the main stream since
-                self.ops.lib.pg_event_arm(None, None)
-                ev.record(torch.cuda.current_stream())
-            ev.wait(self.side)
-        else:
-            self._side_wait_main()
+        self._side_wait_main()
         with torch.cuda.stream(self.side):
-            for _, fn, a, kw in pend:
-                fn(*a, **kw)
-        ev = self._event() or torch.cuda.Event()
+            fn(*a, **kw)
+        ev = self._event(True) or torch.cuda.Event()
         ev.record(self.side)
-        for nets, *_ in pend:
-            for n in nets:
-                self._side_ev[self._dkey if n == "D" else n] = ev
+        for n in nets:
+            self._side_ev[n] = ev
 
     def _side_wait_main(self):
         """The side stream waits for everything enqueued on the current stream so far."""
-        ev = self._event()
+        ev = self._event(False)
         if ev is None:
             self.side.wait_stream(torch.cuda.current_stream())
         else:
@@ -613,16 +574,14 @@ class StepEngine:
             ev.wait(self.side)
 
     def _side_join(self, net=None):
-        """Order the side-stream launches that read `net`'s buffers (all of them when None;
-        "D" = the D buffer set in use) before whatever the current stream enqueues next:
-        called before a pass overwrites a net's activation / gradient buffers, before Adam
-        reads the gradients and at the end of each half-step (so callers reading gradients
-        need no stream handling).  Events, not stream waits: a join never waits for side
-        work of the other buffer set."""
-        self._side_flush()
+        """Order the side-stream launches that read `net`'s buffers (all of them when None)
+        before whatever the current stream enqueues next: called before a pass overwrites a
+        net's activation / gradient buffers, before Adam reads the gradients and at the end of
+        each half-step (so callers reading gradients need no stream handling).  Events, not
+        stream waits: a join never waits for side work of the other net's buffers."""
         if not self._side_ev:
             return
-        keys = list(self._side_ev) if net is None else [self._dkey if net == "D" else net]
+        keys = list(self._side_ev) if net is None else [net]
         cur = torch.cuda.current_stream()
         for k in keys:
             ev = self._side_ev.pop(k, None)
@@ -671,13 +630,13 @@ class StepEngine:
         supports it (the wide LDS-DMA tile at 64^2-256^2): the input-gradient pass forms
         gzb = up2(g) * lrelu'(bits) in the unpool pass (pg_unpool_mask_bits), the R1 tangent
         masks and pools in its conv (no avgpool launch); gzb itself stays materialised for the
-        input-gradient conv and the weight gradient.  PG_UBITS=0: off (A/B runs)."""
+        input-gradient conv and the weight gradient."""
         key = ("ubits", i, 0, 0, 0)
         if key not in self._ws_cache:
             f = self._conv_sup()
             d, Ri, B = self.depths, 8 * 2 ** i, self.B
-            ok = bool(f is not None and self.fuse_dbits and not self._dbits(i) and
-                      os.environ.get("PG_UBITS", "1") != "0" and d[i] % 16 == 0)
+            ok = bool(f is not None and self.fuse_dbits and self.fuse_ubits and
+                      not self._dbits(i) and d[i] % 16 == 0)
             if ok:
                 ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
                         flags=L.CONV_BIAS | L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS)
@@ -686,43 +645,16 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
-    def _abits(self, i):
-        """Whether D level i's conv a also writes the sign bits of its activation (Y2_BITS
-        without the pool) and the two launches that mask with lrelu'(a) -- the conv-b input
-        gradient and the R1 tangent of conv a -- read those bits instead of the bf16
-        activation: 16x fewer mask bytes (the 1024^2 16-channel mask is 134 MB at B = 4).
-        Only at the sign-bit levels (_dbits).  Opt-in (PG_ABITS=1): the masks get cheaper
-        (kbench 1024^2 16->16 74.8 -> 60.5 us, the X_BITS input gradient unchanged) but writing
-        the bits costs the forward conv more (53.2 -> 66.3 us at 1024^2, 34.0 -> 42.8 at
-        512^2), and the step measured 341.7 img/s without vs 338.5 with
-        (profiles/r4_bits_ab.txt)."""
-        key = ("abits", i, 0, 0, 0)
-        if key not in self._ws_cache:
-            f = self._conv_sup()
-            d, Ri, B = self.depths, 8 * 2 ** i, self.B
-            ok = bool(self._dbits(i) and os.environ.get("PG_ABITS", "0") == "1" and
-                      d[i + 1] % 16 == 0)
-            if ok:
-                ok = (f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i + 1],
-                        flags=L.CONV_BIAS | L.CONV_LRELU | L.CONV_Y2_BITS)
-                      and f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i + 1],
-                            flags=L.CONV_MASK | L.CONV_AUX_BITS)
-                      and f(B=B, H=Ri, W=Ri, cin=d[i], cout=d[i + 1],
-                            flags=L.CONV_UPS_IN | L.CONV_X_BITS | L.CONV_AUX_BITS | L.CONV_MASK))
-            self._ws_cache[key] = ok
-        return self._ws_cache[key]
-
     def _rgbbits(self):
         """Whether the top fromRGB layer also writes the sign bits of its output and its two
         lrelu' consumers -- the input gradient of the top conv a and the fromRGB tangent --
-        mask from those bits instead of the bf16 activation (at >= the sign-bit resolution).
-        PG_RGBBITS=0: off (A/B runs)."""
+        mask from those bits instead of the bf16 activation (at >= the sign-bit resolution)."""
         key = ("rgbbits", 0, 0, 0, 0)
         if key not in self._ws_cache:
             f = self._conv_sup()
             d, s, R, B = self.depths, self.s, self.R, self.B
-            ok = bool(f is not None and self.fuse_dbits and s >= 1 and
-                      os.environ.get("PG_RGBBITS", "1") != "0" and d[s] % 8 == 0 and
+            ok = bool(f is not None and self.fuse_dbits and self.fuse_rgbbits and s >= 1 and
+                      d[s] % 8 == 0 and
                       d[s] <= 64 and R >= self.dbits_min_res and
                       f(B=B, H=R, W=R, cin=d[s], cout=d[s], flags=L.CONV_MASK | L.CONV_AUX_BITS))
             self._ws_cache[key] = ok
@@ -731,13 +663,12 @@ class StepEngine:
     def _pn_pool(self, i):
         """Whether level i's conv-a input gradient (pooled to level i-1) also applies level
         i-1's conv-b PixelNorm + LReLU backward (PG_CONV_POOL | PG_CONV_PNBWD): level i-1's
-        forward kept y and r (fused PixelNorm) and the kernel supports it (32 channels).
-        PG_PN_POOL=0: off (A/B runs)."""
+        forward kept y and r (fused PixelNorm) and the kernel supports it (32 channels)."""
         key = ("pnpool", i, 0, 0, 0)
         if key not in self._ws_cache:
             f = getattr(self.ops, "conv_supported", None)
             d, Ri, B = self.depths, 8 * 2 ** i, self.B
-            ok = bool(i >= 1 and f is not None and os.environ.get("PG_PN_POOL", "1") != "0" and
+            ok = bool(i >= 1 and f is not None and self.fuse_pn_pool and
                       self._pn_fused(Ri // 2, d[i], d[i], L.CONV_LRELU) and
                       f(B=B, H=Ri, W=Ri, cin=d[i + 1], cout=d[i],
                         flags=L.CONV_POOL | L.CONV_PNBWD))
@@ -855,7 +786,7 @@ class StepEngine:
         # (pg_rgb_out_bwd_pn: the 16-channel 1024^2 dL/dy never goes through HBM); its weight
         # gradient on the side stream
         top_pn = (s >= 1 and not low and hasattr(ops, "rgb_out_bwd_pn") and d[s] in (16, 32) and
-                  os.environ.get("PG_RGB_PNBWD", "1") != "0" and
+                  self.fuse_rgb_pnbwd and
                   self._pn_fused(self.R, d[s], d[s], L.CONV_LRELU))
         w_rgb = P[pre + "weight"]
         if top_pn:
@@ -936,11 +867,7 @@ class StepEngine:
         h = D["yrgb"]
         for i in reversed(range(s)):                                           # :260-265
             Ri = 8 * 2 ** i
-            if self._abits(i):
-                self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1],
-                           L.CONV_LRELU | L.CONV_Y2_BITS, y2=D[f"ab{i}"])
-            else:
-                self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
+            self._conv("D", f"a{i}", h, D[f"a{i}"], Ri, d[i + 1], d[i + 1], L.CONV_LRELU)
             if self._dbits(i):
                 self._conv("D", f"b{i}", D[f"a{i}"], D[f"p{i}"], Ri, d[i + 1], d[i],
                            L.CONV_LRELU | L.CONV_POOL | L.CONV_Y2_BITS, y2=D[f"mb{i}"],
@@ -982,7 +909,6 @@ class StepEngine:
         # GradExchange) gets that wait as a hook it runs only when it launches a collective:
         # most layers only add to a bucket, and each main-stream event record costs the main
         # stream's next kernel ~6.5 us.
-        self._side_flush()
         main = torch.cuda.current_stream()
         owner = getattr(self.grad_ready, "__self__", None)
         if owner is None or not hasattr(owner, "before_launch"):
@@ -992,7 +918,7 @@ class StepEngine:
             return
 
         def sync():
-            ev = self._event()
+            ev = self._event(False)
             if ev is None:
                 self.side.wait_stream(main)
             else:
@@ -1059,11 +985,8 @@ class StepEngine:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
                                 db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc)
                     ready(b)
-                ab = self._abits(i)
                 self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
-                           L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS |
-                           (L.CONV_AUX_BITS if ab else 0),
-                           aux=D[f"ab{i}"] if ab else D[f"a{i}"],
+                           L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
                            dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
             else:
                 if self._ubits(i):
@@ -1174,12 +1097,8 @@ class StepEngine:
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
-            if self._abits(i):
-                self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1],
-                           L.CONV_MASK | L.CONV_AUX_BITS, aux=D[f"ab{i}"], bias=False)
-            else:
-                self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
-                           aux=D[f"a{i}"], bias=False)
+            self._conv("D", f"a{i}", t, D[f"ta{i}"], Ri, d[i + 1], d[i + 1], L.CONV_MASK,
+                       aux=D[f"a{i}"], bias=False)
             self._wgrad("D", f"a{i}", t, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1], d[i + 1])
             if self._dbits(i):
                 # tangent through conv b, lrelu' (bits) and the avg pool in one launch; the
@@ -1237,10 +1156,6 @@ class StepEngine:
         self.loss[4:5].zero_()
         if self._merged():
             return self._d_step_merged(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake, gp_eps)
-        conc = self.fstream is not None and hp.gp_mode == "r1"
-        if conc:
-            ev0 = torch.cuda.Event()   # the fake pass starts from here, beside the real part
-            ev0.record(torch.cuda.current_stream())
         if self._low(alpha_D):
             ops.img_fade(real, alpha_D, D["real_in"])                       # :217-221
             xr = D["real_in"]
@@ -1254,9 +1169,6 @@ class StepEngine:
             tout, inj = self.d_tangent(PD, GD, gbar, D["u"], alpha_D)
             ops.mul_add(D["u"], tout.view(-1), D["hl"], D["u2"])
             self.d_backward(PD, GD, D["u2"], alpha_D, img=xr, inj_mbstd=inj)
-            if conc:
-                img_fake = self._fake_pass_concurrent(PG, PD, z, alpha_G, alpha_D, ev0, before_fake)
-                return xr, img_fake
         else:
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], None)
@@ -1284,7 +1196,6 @@ class StepEngine:
         separate schedule, which does not read G; the merged forward needs the fake image
         first)."""
         return (self.dd2 is not None and self.hyper.gp_mode in ("r1", "wgan-gp") and
-                self.fstream is None and
                 not hasattr(self._pending_G, "wait"))
 
     @contextlib.contextmanager
@@ -1391,45 +1302,6 @@ class StepEngine:
         self._side_join()
         return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
 
-    def _fake_pass_concurrent(self, PG, PD, z, alpha_G, alpha_D, ev0, before_fake):
-        """The fake-image part of the D half on self.fstream with the second buffer set
-        (see __init__); its D gradients go to a second flat buffer that is added into D's
-        after both parts (per-parameter sums in a different order than the one-stream
-        schedule: within fp32 rounding).  The main stream waits for it on return."""
-        main, fs = torch.cuda.current_stream(), self.fstream
-        gd2 = self.__dict__.get("_gd2")
-        if gd2 is None or gd2[0] is not self.fpD:
-            buf = torch.zeros_like(self.fpD.grad)
-            gd2 = self._gd2 = (self.fpD, buf, {n: self.fpD._view(buf, n) for n in self.fpD.names})
-        _, buf, views = gd2
-        self._side_flush()     # queued launches belong to the main pass's side stream
-        saved = (self.dd, self.ws, self.side, self.ws_side, self._dkey)
-        fs.wait_event(ev0)
-        with torch.cuda.stream(fs):
-            if before_fake is not None:
-                before_fake()      # a deferred Adam_G (+ G packing) only orders the G forward
-            self.dd, self.ws, self.side, self.ws_side, self._dkey = (
-                self.dd_f, self.ws_f, self.side2, self.ws_side2, "Df")
-            try:
-                D = self.dd
-                buf.zero_()
-                img_fake = self.g_forward(PG, z, alpha_G, keep=False)           # :226-227
-                if self.keep_fake_D:
-                    img_fake = img_fake.clone()
-                self.d_forward(PD, img_fake, alpha_D)                           # :228
-                self.ops.bce(D["logit"], False, 1.0, self.loss[1:2], D["u"], None)
-                # per-layer grad_ready is off here: the D gradient is final only after the sum
-                self.d_backward(PD, views, D["u"], alpha_D, img=img_fake, final=False)
-                self._side_join("D")
-            finally:
-                self.ws_f, self.ws_side2 = self.ws, self.ws_side
-                self.dd, self.ws, self.side, self.ws_side, self._dkey = saved
-        main.wait_stream(fs)
-        self._side_join()
-        n = self.fpD.n_live
-        self._GD_flat[:n].add_(buf[:n])
-        return img_fake
-
     def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
         """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm.
         Fused form: the interpolation eps x_r + (1 - eps) x_f is read by the fromRGB layers
@@ -1515,19 +1387,6 @@ class StepEngine:
                       beta2=hp.beta2, eps=hp.eps, step=fp.step)
 
     def train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
-        """_train_step on the high-priority main stream when PG_MAIN_PRIORITY=1 (see
-        __init__), ordered after and back into the caller's stream."""
-        hs = self.main_hp
-        if hs is None or torch.cuda.is_current_stream_capturing():
-            return self._train_step(real, z1, z2, alpha_G, alpha_D, grad_hook, gp_eps)
-        cur = torch.cuda.current_stream()
-        hs.wait_stream(cur)
-        with torch.cuda.stream(hs):
-            out = self._train_step(real, z1, z2, alpha_G, alpha_D, grad_hook, gp_eps)
-        cur.wait_stream(hs)
-        return out
-
-    def _train_step(self, real, z1, z2, alpha_G, alpha_D, grad_hook=None, gp_eps=None):
         """One full step: D half (R1) + Adam_D, G half + Adam_G (pggan/model.py:206-255).
 
         grad_hook(net, flat_live_grad) runs before each Adam (DP all-reduce).  If it returns

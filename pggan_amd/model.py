@@ -139,10 +139,10 @@ class ProgressiveGAN:
             from .dp import GradExchange
             rd = torch.bfloat16 if cfg_get(self.args, "dp_reduce_dtype", "f32") == "bf16" \
                 else torch.float32
-            # bucket size: PG_DP_BUCKET_MB (tuning) > config dp_bucket_mb > 32 MiB.  Each
-            # collective costs ~50-100 us of host time (torch + RCCL enqueue); 4 MiB buckets
-            # made the host enqueue the step's bound (bench.py --dp-exchange)
-            mb = float(os.environ.get("PG_DP_BUCKET_MB", cfg_get(self.args, "dp_bucket_mb", 32)))
+            # bucket size: config dp_bucket_mb (32 MiB).  Each collective costs ~50-100 us of
+            # host time (torch + RCCL enqueue); 4 MiB buckets made the host enqueue the step's
+            # bound (bench.py --dp-exchange)
+            mb = float(cfg_get(self.args, "dp_bucket_mb", 32))
             self._exchange = GradExchange(self.world, bucket_bytes=int(mb * (1 << 20)),
                                           reduce_dtype=rd)
 
@@ -288,12 +288,12 @@ class ProgressiveGAN:
             eng.flush()
 
     # one training step captured once per (stage, schedule scalars) and replayed as a
-    # hipGraph (world == 1, PG_GRAPH=1): the host enqueue of ~600 launches (6.3 ms) becomes
+    # hipGraph (world == 1, use_graph = True): the host enqueue of ~600 launches (6.3 ms) becomes
     # one graph launch (1.5-1.7 ms).  Off by default: on ROCm 7.2 the replay of this
     # two-stream step runs 6-7 % slower on the GPU than the eager streams (13.5 vs 12.55
     # ms/step, interleaved A/B in one call, profiles/r3_graph_ab.txt), and the step is
     # GPU-bound (12.5 ms of kernels vs 6.3 ms of host enqueue).
-    use_graph = os.environ.get("PG_GRAPH", "0") == "1"
+    use_graph = False
     graph_replays = 0
 
     def _graph_key(self, eng, B):

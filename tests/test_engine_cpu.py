@@ -16,7 +16,7 @@ from pggan_amd import engine as E
 NAMES = [c[0] for c in GOLDEN_CONFIGS]
 
 
-def build(meta, ops, device="cpu"):
+def build(meta, ops, device="cpu", **opts):
     depths, s, B = meta["depths"], meta["s"], meta["B"]
     gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
     PG = make_params(gsh, seed=1000 + 10 * s + B)
@@ -25,7 +25,7 @@ def build(meta, ops, device="cpu"):
                        {k: torch.from_numpy(v) for k, v in PG.items()})
     fpD = E.FlatParams(dsh, E.dead_params("D", s), device,
                        {k: torch.from_numpy(v) for k, v in PD.items()})
-    eng = E.StepEngine(ops, depths, s, B, device)
+    eng = E.StepEngine(ops, depths, s, B, device, **opts)
     if device == "cpu":
         # exercise both sign-bit schedules at the fixture sizes: 8^2 keeps the conv-b bits for
         # the unpool pass (_ubits), >= 16^2 the full sign-bit path (_dbits)
@@ -75,15 +75,25 @@ def test_engine_schedule_unfused_pixelnorm():
 
 
 @pytest.mark.parametrize("name", ["tiny_s3_b4_a1", "tiny_s1_b4_a05"])
-def test_engine_schedule_merged_generator_forward(name, monkeypatch):
-    """The opt-in merged generator forward (PG_MERGE_G=1: both G forwards of a step at
-    batch 2B, the G half reading the second-half views) against the golden fixtures."""
-    monkeypatch.setenv("PG_MERGE_G", "1")
+def test_engine_schedule_separate_generator_forwards(name):
+    """Merged D passes with the G half's own generator forward (merge_g=False: the schedule
+    the engine falls back to under a bucketed DP exchange) against the golden fixtures; the
+    default (both generator forwards merged at batch 2B) is test_engine_schedule_matches_reference."""
     torch.set_num_threads(4)
     meta, z = load(name)
-    eng, fpG, fpD = build(meta, CpuOps())
-    assert eng.g2 is not None and eng.dd2 is not None
+    eng, fpG, fpD = build(meta, CpuOps(), merge_g=False)
+    assert eng.g2 is None and eng.dd2 is not None
     run_and_check(meta, z, eng, fpG, fpD, tol=1e-3)
+
+
+def test_engine_options_env(monkeypatch):
+    """PG_ENGINE (A/B runs) overrides the schedule defaults; unknown names raise."""
+    monkeypatch.setenv("PG_ENGINE", "merge_g=0,dbits_min_res=64")
+    o = E.engine_options()
+    assert o["merge_g"] is False and o["dbits_min_res"] == 64 and o["merge_d"] is True
+    monkeypatch.setenv("PG_ENGINE", "no_such_option=1")
+    with pytest.raises(ValueError):
+        E.engine_options()
 
 
 GP_NAMES = ["gp_tiny_s2_b8_a03", "gp_tiny_s1_b4_a05"]
@@ -129,40 +139,53 @@ def test_engine_wgan_gp_step(name):
     run_gp_and_check(name, CpuOps())
 
 
+def run_steps(ops_factory, device, depths, s, B, steps=2, elide=True):
+    """`steps` training steps at alpha = 1 from fixed parameters and inputs: per step the
+    three images, the loss vector, both flat gradients and both flat parameter buffers."""
+    gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
+    PG = {k: torch.from_numpy(v) for k, v in make_params(gsh, seed=61).items()}
+    PD = {k: torch.from_numpy(v) for k, v in make_params(dsh, seed=62).items()}
+    fpG = E.FlatParams(gsh, E.dead_params("G", s), device, PG)
+    fpD = E.FlatParams(dsh, E.dead_params("D", s), device, PD)
+    eng = E.StepEngine(ops_factory(), depths, s, B, device)
+    eng.elide_zero_blend = elide
+    eng.bind(fpG, fpD, E.Hyper())
+    eng.keep_fake_D = True
+    res = []
+    for t, st in enumerate(make_inputs(B, 4 * 2 ** s, seed=63, n_steps=steps)):
+        r, z1, z2 = (torch.from_numpy(st[k]).to(device) for k in ("real", "z1", "z2"))
+        ims = eng.train_step(r, z1, z2, 1.0, 1.0)
+        eng.flush()
+        res.append([x.detach().cpu().clone() for x in ims] +
+                   [eng.loss.cpu().clone(), fpD.grad.cpu().clone(), fpG.grad.cpu().clone(),
+                    fpD.flat.cpu().clone(), fpG.flat.cpu().clone()])
+    return res
+
+
+STEP_TENSORS = ["img_real", "img_fake_D", "img_fake_G", "loss", "grad_D", "grad_G", "param_D",
+                "param_G"]
+
+
+def assert_runs_equal(out_a, out_b, rtol=0.0):
+    """Per step and tensor: bitwise equal (rtol 0) or within rtol relative L2."""
+    for t, (a, b) in enumerate(zip(out_a, out_b)):
+        for name, x, y in zip(STEP_TENSORS, a, b):
+            if rtol == 0.0:
+                assert torch.equal(x, y), (f"step {t} {name}: {int((x != y).sum())} elements differ, "
+                                           f"max {float((x - y).abs().max())}")
+            else:
+                e = float((x.double() - y.double()).norm() / max(float(y.double().norm()), 1e-30))
+                assert e <= rtol, (t, name, e)
+
+
 def elision_bitwise(ops_factory, device, depths, s, B, dtype=torch.float32, steps=2, rtol=0.0):
     """alpha = 1: eliding the fade-in's exactly-zero low-resolution branches (engine
     .elide_zero_blend) must leave every image, loss, gradient and parameter bit-identical
     to computing them (the reference computes them, pggan/nets.py:155-156,263-265).
-    rtol > 0: the HIP step's cross-workgroup fp32 atomics (R1 sum, to/fromRGB weight
-    gradients, split slab sums) are not bitwise reproducible run to run, so there the two
-    runs are held to rtol per tensor instead."""
-    out = []
-    for elide in (False, True):
-        gsh, dsh = E.g_param_shapes(depths, s), E.d_param_shapes(depths, s)
-        PG = {k: torch.from_numpy(v) for k, v in make_params(gsh, seed=61).items()}
-        PD = {k: torch.from_numpy(v) for k, v in make_params(dsh, seed=62).items()}
-        fpG = E.FlatParams(gsh, E.dead_params("G", s), device, PG)
-        fpD = E.FlatParams(dsh, E.dead_params("D", s), device, PD)
-        eng = E.StepEngine(ops_factory(), depths, s, B, device)
-        eng.elide_zero_blend = elide
-        eng.bind(fpG, fpD, E.Hyper())
-        eng.keep_fake_D = True
-        res = []
-        for t, st in enumerate(make_inputs(B, 4 * 2 ** s, seed=63, n_steps=steps)):
-            r, z1, z2 = (torch.from_numpy(st[k]).to(device) for k in ("real", "z1", "z2"))
-            ims = eng.train_step(r, z1, z2, 1.0, 1.0)
-            eng.flush()
-            res.append([x.detach().cpu().clone() for x in ims] +
-                       [eng.loss.cpu().clone(), fpD.grad.cpu().clone(), fpG.grad.cpu().clone(),
-                        fpD.flat.cpu().clone(), fpG.flat.cpu().clone()])
-        out.append(res)
-    for t, (a, b) in enumerate(zip(*out)):
-        for i, (x, y) in enumerate(zip(a, b)):
-            if rtol == 0.0:
-                assert torch.equal(x, y), (t, i, float((x - y).abs().max()))
-            else:
-                e = float((x.double() - y.double()).norm() / max(float(y.double().norm()), 1e-30))
-                assert e <= rtol, (t, i, e)
+    rtol > 0: where the elided schedule runs different (fused) kernels than the computed
+    one -- bf16 storage, whose roundings then differ -- the two are held to rtol per tensor."""
+    out = [run_steps(ops_factory, device, depths, s, B, steps, elide) for elide in (False, True)]
+    assert_runs_equal(out[0], out[1], rtol)
 
 
 def test_alpha_one_elision_is_bitwise():

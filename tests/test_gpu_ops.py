@@ -76,8 +76,7 @@ CONV_CASES = [
     (4, 128, 64, 128, ("bias", "lrelu")),
     (8, 128, 64, 64, ("ups", "bias", "lrelu", "pool")),
     (4, 128, 128, 128, ("mask", "accum")),
-    # tile 3 with more tiles than one round of workgroups (the default one-tile-per-workgroup
-    # launch; the opt-in persistent form, PG_HR_MT=1: test_conv3x3_fwd_opt_in): one chunk
+    # tile 3 with more tiles than one round of workgroups (one tile per workgroup): one chunk
     # with the pre-pool copy, two chunks x two output-channel blocks, two chunks with bias
     (4, 256, 32, 64, ("bias", "lrelu", "pool")),
     (2, 256, 64, 128, ("mask", "accum")),
@@ -151,8 +150,7 @@ WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, Fa
                # bench-like: many pixel splits (slabs), direct single split, ups + cin 32
                (4, 128, 16, 32, False), (4, 32, 512, 512, False), (2, 64, 32, 16, True),
                (4, 64, 64, 128, False),
-               # the 16^2 wide layer (the register-staged kernel by default; the opt-in LDS-DMA
-               # form, PG_WG_DMA16=1: test_conv3x3_wgrad_dma16_opt_in) and the LDS-DMA kernel with ups
+               # the 16^2 wide layer (the register-staged kernel) and the LDS-DMA kernel with ups
                (4, 16, 512, 512, False), (2, 64, 256, 128, True)]
 
 
@@ -424,9 +422,9 @@ def test_conv3x3_splitk(case, dtype):
         cmp(outs[0][1], outs[1][1], tol_for(dtype), "splitk y2")
 
 
-KG_CASES = [
-    # the K-grouped wide kernel (conv_kg.hip): 8-row tiles at 32^2 (3-slot ring), 16-row at
-    # 64^2, 32-row at >= 128^2; every epilogue it takes
+WIDE_CASES = [
+    # wide bf16 convs at 32^2-512^2 through the default dispatch (tiles 13 / 6 / 3 / 14 and the
+    # persistent narrow tiles) with every epilogue they take
     (4, 32, 512, 512, ("bias", "lrelu")),
     (4, 32, 512, 512, ("mask", "accum")),
     (4, 32, 512, 512, ("bias", "lrelu", "pool")),
@@ -448,12 +446,10 @@ KG_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", KG_CASES)
-def test_conv_kg(case, monkeypatch):
-    """bf16 wide convs through the K-grouped kernel (opt-in; PG_KG=2 takes it for every eligible
-    shape) against the CPU double: output, the pre-pool copy (y2 with POOL) and the PixelNorm
-    factor (y2 with PIXNORM)."""
-    monkeypatch.setenv("PG_KG", "2")
+@pytest.mark.parametrize("case", WIDE_CASES)
+def test_conv_wide(case):
+    """bf16 wide convs against the CPU double: output, the pre-pool copy (y2 with POOL) and
+    the PixelNorm factor (y2 with PIXNORM)."""
     B, H, cin, cout, fl = case
     _L = lib()
     dtype = torch.bfloat16
@@ -487,28 +483,9 @@ def test_conv_kg(case, monkeypatch):
                     slope=0.2, out_scale=0.25 if "pool" in fl else 1.0,
                     bias=(bias * scale).to(dev), aux=aux.to(dev).to(dt), y2=y2)
         outs.append((y, y2))
-    cmp(outs[0][0], outs[1][0], 2e-2, "kg y")
+    cmp(outs[0][0], outs[1][0], 2e-2, "wide y")
     if outs[0][1] is not None:
-        cmp(outs[0][1], outs[1][1], 2e-2, "kg y2")
-
-
-@pytest.mark.parametrize("knob,case", [
-    # the opt-in persistent multi-tile form of tile 3 (PG_HR_MT=1): more tiles than one round
-    ("PG_HR_MT", (4, 256, 32, 64, ("bias", "lrelu", "pool"))),
-    ("PG_HR_MT", (2, 256, 64, 128, ("mask", "accum"))),
-    ("PG_HR_MT", (4, 256, 64, 64, ("bias", "lrelu"))),
-])
-def test_conv3x3_fwd_opt_in(knob, case, monkeypatch):
-    """The off-by-default kernels that ship in the library, switched on per call."""
-    monkeypatch.setenv(knob, "1")
-    test_conv3x3_fwd(case, torch.bfloat16)
-
-
-@pytest.mark.parametrize("case", [(4, 16, 512, 512, False)])
-def test_conv3x3_wgrad_dma16_opt_in(case, monkeypatch):
-    """The LDS-DMA weight gradient at 16^2 (PG_WG_DMA16=1, off by default)."""
-    monkeypatch.setenv("PG_WG_DMA16", "1")
-    test_conv3x3_wgrad(case, torch.bfloat16, True)
+        cmp(outs[0][1], outs[1][1], 2e-2, "wide y2")
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
