@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--no-kernel-events", action="store_true")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a hipGraph from the second step on (one process)")
+    p.add_argument("--replay", action="store_true",
+                   help="record the step with the library's launch recorder and replay it from "
+                        "C++ from the third step on (one process)")
     p.add_argument("--dp-exchange", action="store_true",
                    help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
                         "group), to measure the bookkeeping's cost against the plain step")
@@ -352,6 +355,9 @@ def main():
     # --graph (one process): from the second step on, train_step replays the step captured
     # as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
     model.use_graph = bool(args.graph)
+    # --replay (one process): the step recorded by the library from the second step on and
+    # re-issued from C++ (pg_replay) on the engine's own streams
+    model.use_replay = bool(args.replay) and world == 1 and not args.dp_exchange
     for _ in range(args.warmup):
         step()
     model.flush()
@@ -377,7 +383,7 @@ def main():
         # launch), the others are graph replays.
         if timer and i == args.steps - 1:
             timer.on = True
-            model.use_graph = False
+            model.use_graph = model.use_replay = False
         step()
     model.flush()        # the last step's (deferred) generator update is part of the step
     torch.cuda.synchronize()

@@ -380,6 +380,27 @@ int pg_stream_create(int lowest_priority, void** stream);
 int pg_stream_destroy(void* stream);
 int pg_event_destroy(void* ev);
 
+/* ---- device memory helpers that take part in recordings: zero `bytes` at p / copy `bytes`
+ * device to device, asynchronously on `stream` (the step's gradient and loss resets and its
+ * input copies, so a recorded step needs no torch op) */
+int pg_fill_zero(void* p, size_t bytes, void* stream);
+int pg_copy(void* dst, const void* src, size_t bytes, void* stream);
+
+/* ---- launch recorder (the training step replayed from C++; reference hot loop train.py:39-66).
+ * Between pg_record_begin and pg_record_end every kernel launch, pg_event_record,
+ * pg_stream_wait_event, pg_fill_zero and pg_copy this host thread issues runs as usual AND is
+ * appended to a recording (function, geometry, stream, arguments by value).  pg_replay issues
+ * the same sequence again on the same streams: one C++ loop instead of the Python layer that
+ * produced it, and -- unlike a hipGraph -- the streams and their hardware queues are the
+ * recorded ones.  The caller guarantees that every pointer the recording holds still points to
+ * the same live buffers and that their contents (inputs, step counters) are meant to be
+ * re-read; a recording is replayed on the thread's current device.  Handles are opaque. */
+int pg_record_begin(void);
+int pg_record_end(void** rec);
+int pg_record_count(const void* rec);
+int pg_replay(const void* rec);
+void pg_record_destroy(void* rec);
+
 /* ---- step plan: the kernel path of every 3x3 conv pass (forward, input
  * gradient, weight gradient) of one train_step at (stage, batch, dtype) -- the layer list of
  * pggan/nets.py:53-119 (G) and :164-239 (D) at scale_index = stage -- and the split-reduction

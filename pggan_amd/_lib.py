@@ -162,6 +162,13 @@ _SIGS = {
     "pg_stream_wait_event": ([_VP, _VP], _I),
     "pg_event_elapsed_ms": ([_VP, _VP, ctypes.POINTER(ctypes.c_float)], _I),
     "pg_event_destroy": ([_VP], _I),
+    "pg_fill_zero": ([_VP, _SZ, _VP], _I),
+    "pg_copy": ([_VP, _VP, _SZ, _VP], _I),
+    "pg_record_begin": ([], _I),
+    "pg_record_end": ([ctypes.POINTER(ctypes.c_void_p)], _I),
+    "pg_record_count": ([_VP], _I),
+    "pg_replay": ([_VP], _I),
+    "pg_record_destroy": ([_VP], None),
     "pg_stream_create": ([_I, ctypes.POINTER(ctypes.c_void_p)], _I),
     "pg_stream_destroy": ([_VP], _I),
 }
@@ -232,6 +239,28 @@ class HipEvent:
                 pass
 
 
+class Recording:
+    """A pg_record_* recording: replay() issues the recorded launches again (pg_replay)."""
+
+    def __init__(self, ops, h):
+        self.lib, self.h = ops.lib, h
+        self.ops = ops
+
+    def __len__(self):
+        return int(self.lib.pg_record_count(self.h))
+
+    def replay(self):
+        self.ops._chk(self.lib.pg_replay(self.h), "replay")
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h is not None and h.value:
+            try:
+                self.lib.pg_record_destroy(h)
+            except Exception:
+                pass
+
+
 class HipOps:
     """Tensor-level wrappers of the C ABI.  `dtype` = storage dtype of activations."""
 
@@ -286,6 +315,31 @@ class HipOps:
     def event(self, timing=False):
         """A HipEvent (device-scope release; see pg_event_create)."""
         return HipEvent(self, timing)
+
+    # -- device memory (recordable) ------------------------------------------
+    def zero_(self, t):
+        """t.zero_() through the library (pg_fill_zero: part of a recording)."""
+        self._cuda(t)
+        assert t.is_contiguous()
+        self._chk(self.lib.pg_fill_zero(_p(t), t.numel() * t.element_size(), self._s()), "fill_zero")
+
+    def copy_(self, dst, src):
+        """dst.copy_(src) for same-dtype contiguous device tensors (pg_copy: recordable)."""
+        self._cuda(dst, src)
+        assert dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype
+        assert dst.numel() == src.numel()
+        self._chk(self.lib.pg_copy(_p(dst), _p(src), dst.numel() * dst.element_size(), self._s()),
+                  "copy")
+
+    # -- launch recorder (include/pggan_hip.h: pg_record_*) ------------------
+    def record_begin(self):
+        self._chk(self.lib.pg_record_begin(), "record_begin")
+
+    def record_end(self):
+        """The launches since record_begin as a Recording (replay() re-issues them)."""
+        h = ctypes.c_void_p()
+        self._chk(self.lib.pg_record_end(ctypes.byref(h)), "record_end")
+        return Recording(self, h)
 
     # -- step plan ---------------------------------------------------------
     def step_plan(self, depths, stage, batch):

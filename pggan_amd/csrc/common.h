@@ -293,8 +293,41 @@ void pg_set_error(const char* fmt, ...);
     }                                       \
   } while (0)
 
-// Every kernel launch of the library goes through PG_KLAUNCH.
-#define PG_KLAUNCH(K, G, B, L, S, ...) hipLaunchKernelGGL(K, G, B, L, (S), __VA_ARGS__)
+// ---- launches and the launch recorder ---------------------------------------
+// Every kernel launch of the library goes through PG_KLAUNCH -> pg_launch: the arguments are
+// converted to the kernel's parameter types once, and the launch is a hipLaunchKernel over
+// them.  While the calling host thread records (pg_record_begin .. pg_record_end), the launch
+// is also appended to the recording -- function, geometry, stream and the converted argument
+// tuple by value -- so pg_replay can issue the same sequence again from C++ on the same streams
+// (the host enqueue of a ~380-launch training step without its Python layer, and without
+// hipGraph's re-levelling of the two streams onto other hardware queues).
+#include <functional>
+#include <tuple>
+#include <utility>
+
+bool pg_recording();
+void pg_record_push(std::function<hipError_t()> op);
+extern "C" int pg_fill_zero(void* p, size_t bytes, void* stream);
+
+template <typename... KArgs, size_t... I>
+inline hipError_t pg_launch_tuple(void (*k)(KArgs...), dim3 g, dim3 b, unsigned lds, hipStream_t s,
+                                  std::tuple<KArgs...>& t, std::index_sequence<I...>) {
+  void* argv[sizeof...(KArgs) + 1] = {(void*)&std::get<I>(t)...};
+  return hipLaunchKernel((const void*)k, g, b, argv, lds, s);
+}
+
+template <typename... KArgs, typename... Args>
+inline void pg_launch(void (*k)(KArgs...), dim3 g, dim3 b, unsigned lds, hipStream_t s,
+                      Args&&... args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "pg_launch: kernel argument count");
+  std::tuple<KArgs...> t{static_cast<KArgs>(std::forward<Args>(args))...};
+  (void)pg_launch_tuple(k, g, b, lds, s, t, std::index_sequence_for<KArgs...>{});
+  if (pg_recording())
+    pg_record_push([=]() mutable {
+      return pg_launch_tuple(k, g, b, lds, s, t, std::index_sequence_for<KArgs...>{});
+    });
+}
+#define PG_KLAUNCH(K, G, B, L, S, ...) pg_launch((K), dim3(G), dim3(B), (L), (S), __VA_ARGS__)
 
 #define PG_LAUNCH_CHECK()                                                       \
   do {                                                                          \

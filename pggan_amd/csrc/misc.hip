@@ -6,6 +6,7 @@
 // fp32 arithmetic, one pass over each tensor.
 #include <cstdarg>
 #include <cstdio>
+#include <vector>
 
 #include "common.h"
 
@@ -17,6 +18,14 @@ void pg_set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+// the launch recorder (common.h: pg_launch; include/pggan_hip.h: pg_record_*)
+struct PgRecording {
+  std::vector<std::function<hipError_t()>> ops;
+};
+static thread_local PgRecording* g_rec = nullptr;
+bool pg_recording() { return g_rec != nullptr; }
+void pg_record_push(std::function<hipError_t()> op) { g_rec->ops.push_back(std::move(op)); }
 
 namespace {
 
@@ -1847,7 +1856,8 @@ int pg_gp_penalty(int B, size_t per, const float* g, float w, float* gp_out, flo
                   float* gbar, void* scratch, void* stream) {
   PG_CHECK_ARG(g && gp_out && norms && gbar && scratch, "gp_penalty: bad args (scratch required)");
   hipStream_t st = (hipStream_t)stream;
-  (void)hipMemsetAsync(norms, 0, sizeof(float) * B, st);
+  const int zrc = pg_fill_zero(norms, sizeof(float) * B, st);
+  if (zrc != PG_OK) return zrc;
   int gx = grid_for(per, 256, 256);
   PG_CHECK_ARG(pg_det_fits((size_t)gx * B, 1), "gp_penalty: B too large for the scratch");
   PG_KLAUNCH(sumsq_per_sample_kernel, dim3(gx, B), dim3(256), 0, st, B, per, g, norms,
@@ -1956,14 +1966,66 @@ int pg_event_create(int timing, void** ev) {
 
 int pg_event_record(void* ev, void* stream) {
   PG_CHECK_ARG(ev, "event_record: null event");
-  return pg_hip_status(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream), "hipEventRecord");
+  hipEvent_t e = (hipEvent_t)ev;
+  hipStream_t st = (hipStream_t)stream;
+  if (pg_recording()) pg_record_push([=]() { return hipEventRecord(e, st); });
+  return pg_hip_status(hipEventRecord(e, st), "hipEventRecord");
 }
 
 int pg_stream_wait_event(void* stream, void* ev) {
   PG_CHECK_ARG(ev, "stream_wait_event: null event");
-  return pg_hip_status(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0),
-                       "hipStreamWaitEvent");
+  hipEvent_t e = (hipEvent_t)ev;
+  hipStream_t st = (hipStream_t)stream;
+  if (pg_recording()) pg_record_push([=]() { return hipStreamWaitEvent(st, e, 0); });
+  return pg_hip_status(hipStreamWaitEvent(st, e, 0), "hipStreamWaitEvent");
 }
+
+int pg_fill_zero(void* p, size_t bytes, void* stream) {
+  PG_CHECK_ARG(p || !bytes, "fill_zero: null pointer");
+  if (!bytes) return PG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (pg_recording()) pg_record_push([=]() { return hipMemsetAsync(p, 0, bytes, st); });
+  return pg_hip_status(hipMemsetAsync(p, 0, bytes, st), "hipMemsetAsync");
+}
+
+int pg_copy(void* dst, const void* src, size_t bytes, void* stream) {
+  PG_CHECK_ARG((dst && src) || !bytes, "copy: null pointer");
+  if (!bytes || dst == src) return PG_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (pg_recording())
+    pg_record_push([=]() { return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st); });
+  return pg_hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+}
+
+int pg_record_begin(void) {
+  PG_CHECK_ARG(!g_rec, "record_begin: this thread is already recording");
+  g_rec = new PgRecording();
+  return PG_OK;
+}
+
+int pg_record_end(void** rec) {
+  PG_CHECK_ARG(rec, "record_end: null out");
+  PG_CHECK_ARG(g_rec, "record_end: not recording");
+  *rec = g_rec;
+  g_rec = nullptr;
+  return PG_OK;
+}
+
+int pg_record_count(const void* rec) {
+  return rec ? (int)static_cast<const PgRecording*>(rec)->ops.size() : 0;
+}
+
+int pg_replay(const void* rec) {
+  PG_CHECK_ARG(rec, "replay: null recording");
+  PG_CHECK_ARG(!g_rec, "replay: not while recording");
+  for (const auto& op : static_cast<const PgRecording*>(rec)->ops) {
+    const hipError_t e = op();
+    if (e != hipSuccess) return pg_hip_status(e, "replay");
+  }
+  return PG_OK;
+}
+
+void pg_record_destroy(void* rec) { delete static_cast<PgRecording*>(rec); }
 
 int pg_event_elapsed_ms(void* ev_start, void* ev_end, float* ms) {
   PG_CHECK_ARG(ev_start && ev_end && ms, "event_elapsed_ms: null argument");

@@ -15,6 +15,15 @@ ColorJitter.get_params: `torch.randperm(4)`, brightness, contrast, saturation, h
 parameters as the reference's transform.  The jitter is the reference's PIL path
 (ImageEnhance blends and PIL's uint8 HSV hue shift, uint8 after every op) in Pillow's own
 arithmetic: the output equals the reference transform byte for byte (tests/test_augment.py).
+
+HBM cache (`HbmImageCache`): decode + Resize is deterministic and runs before every random
+op (lib/dataset.py:102-112), so the resized uint8 image of a dataset index is the same in
+every epoch.  The loader keeps it in HBM after its first decode (per stage: the target size
+changes with the stage) and gathers later batches from there, so after the first epoch the
+host decode -- 344 img/s from 1024^2 PNG on the box's 16 threads, below the step's rate at
+every stage (profiles/r4_loader.json) -- no longer bounds training.  The bytes the augmentation
+reads are the ones it would have decoded, so the output stays byte-exact.  Sizes: 3 S^2 bytes
+per image (3 MiB at 1024^2, 192 KiB at 256^2); a DP rank caches only its own shard.
 """
 from __future__ import annotations
 
@@ -81,12 +90,54 @@ class ImageFolderDataset:
         return load_u8(self.paths[i], self.size)
 
 
+class HbmImageCache:
+    """The decoded + resized uint8 images of one dataset at one size, in HBM: slot table
+    (dataset index -> row of `buf`, -1 = not cached) and rows filled in first-decode order
+    until `budget_bytes` is used (the rest is decoded on the host every time)."""
+
+    def __init__(self, n, size, device, budget_bytes):
+        per = 3 * size * size
+        self.cap = int(max(0, min(n, budget_bytes // per)))
+        self.size = size
+        self.slot = np.full(n, -1, dtype=np.int64)
+        self.used = 0
+        self.buf = (torch.empty(self.cap, size, size, 3, dtype=torch.uint8, device=device)
+                    if self.cap else None)
+
+    def slots(self, idx):
+        return [int(self.slot[i]) for i in idx]
+
+    def insert(self, idx, dev_imgs):
+        """Store rows dev_imgs[k] (uint8 [m, S, S, 3] on the device) for dataset indices idx
+        while there is room; returns how many were stored."""
+        k = 0
+        for j, i in enumerate(idx):
+            if self.slot[i] >= 0 or self.used >= self.cap:
+                continue
+            self.buf[self.used].copy_(dev_imgs[j])
+            self.slot[i] = self.used
+            self.used += 1
+            k += 1
+        return k
+
+
+def default_cache_bytes(device, fraction=0.4):
+    """HBM for the image cache: `fraction` of the device's free memory now."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return 0
+    free, _ = torch.cuda.mem_get_info(dev)
+    return int(free * fraction)
+
+
 class BatchLoader:
     """Decode/resize in `workers` host threads (PIL releases the GIL), one batch ahead;
     flip + jitter + normalize on the GPU.  `next(indices, prefetch=None)` returns the fp32
-    NCHW [-1, 1] batch on `device` and starts decoding `prefetch` (the next indices)."""
+    NCHW [-1, 1] batch on `device` and starts decoding `prefetch` (the next indices).
+    cache_bytes > 0: decoded images are kept in an HbmImageCache and later batches gather
+    them there (no decode, no host-to-device copy); None: default_cache_bytes."""
 
-    def __init__(self, dataset, device, ops, seed=0, workers=None, gen=None):
+    def __init__(self, dataset, device, ops, seed=0, workers=None, gen=None, cache_bytes=None):
         """gen: the torch CPU generator the augmentation parameters are drawn from (shared
         across the loaders of successive stages); default a new one seeded with `seed`."""
         self.ds, self.dev, self.ops = dataset, torch.device(device), ops
@@ -94,27 +145,53 @@ class BatchLoader:
             raise RuntimeError("pggan_amd: the input pipeline needs the HIP library (augment_u8)")
         self.pool = ThreadPoolExecutor(max_workers=workers or min(16, os.cpu_count() or 1))
         self.gen = gen if gen is not None else torch.Generator().manual_seed(seed)
-        self._pending = None     # (indices, futures)
+        self._pending = {}       # dataset index -> future of its decoded image
         self._ws = None
+        if cache_bytes is None:
+            cache_bytes = default_cache_bytes(self.dev)
+        self.cache = (HbmImageCache(len(dataset), dataset.size, self.dev, cache_bytes)
+                      if cache_bytes > 0 else None)
+        self.decoded = 0         # images decoded on the host so far
+
+    def _cached(self, i):
+        return self.cache is not None and self.cache.slot[i] >= 0
 
     def _submit(self, idx):
-        return tuple(idx), [self.pool.submit(self.ds.load, int(i)) for i in idx]
+        for i in idx:
+            i = int(i)
+            if i not in self._pending and not self._cached(i):
+                self._pending[i] = self.pool.submit(self.ds.load, i)
 
     def next(self, idx, prefetch=None):
-        idx = tuple(int(i) for i in idx)
-        if self._pending is None or self._pending[0] != idx:
-            self._pending = self._submit(idx)
-        imgs = [f.result() for f in self._pending[1]]
-        self._pending = self._submit(prefetch) if prefetch is not None else None
-        B, S = len(imgs), self.ds.size
-        host = torch.from_numpy(np.stack(imgs)).pin_memory()
-        src = host.to(self.dev, non_blocking=True)
+        idx = [int(i) for i in idx]
+        self._submit(idx)
+        B, S = len(idx), self.ds.size
+        miss = [k for k, i in enumerate(idx) if not self._cached(i)]
+        src = torch.empty(B, S, S, 3, dtype=torch.uint8, device=self.dev)
+        if miss:
+            imgs = [self._pending.pop(idx[k]).result() for k in miss]
+            self.decoded += len(imgs)
+            host = torch.from_numpy(np.stack(imgs)).pin_memory()
+            dev_miss = host.to(self.dev, non_blocking=True)
+            src[torch.tensor(miss, device=self.dev)] = dev_miss
+            if self.cache is not None:
+                self.cache.insert([idx[k] for k in miss], dev_miss)
+        hit = [k for k in range(B) if k not in miss]
+        if hit:
+            rows = torch.tensor([int(self.cache.slot[idx[k]]) for k in hit], device=self.dev)
+            if len(hit) == B:
+                torch.index_select(self.cache.buf, 0, rows, out=src)
+            else:
+                src[torch.tensor(hit, device=self.dev)] = self.cache.buf.index_select(0, rows)
+        if prefetch is not None:
+            self._submit(prefetch)
         params = torch.from_numpy(draw_params(B, self.gen)).to(self.dev, non_blocking=True)
         out = torch.empty(B, 3, S, S, dtype=torch.float32, device=self.dev)
         self._ws = self.ops.augment_u8(src, params, out, ws=self._ws)
         return out
 
     def close(self):
-        """Stop the decode threads; pending prefetches are cancelled."""
-        self._pending = None
+        """Stop the decode threads; pending prefetches are cancelled; the cache is freed."""
+        self._pending = {}
+        self.cache = None
         self.pool.shutdown(wait=False, cancel_futures=True)

@@ -288,6 +288,21 @@ class StepEngine:
         return ev
 
     # ------------------------------------------------------------------ buffers
+    def _zero(self, t):
+        """t.zero_() through the op set where it offers it (recordable, pg_fill_zero)."""
+        if hasattr(self.ops, "zero_") and t.is_contiguous():
+            self.ops.zero_(t)
+        else:
+            t.zero_()
+
+    def _copy(self, dst, src):
+        """dst.copy_(src) through the op set where possible (recordable, pg_copy)."""
+        if (hasattr(self.ops, "copy_") and dst.is_contiguous() and src.is_contiguous() and
+                dst.dtype == src.dtype and src.is_cuda and dst.numel() == src.numel()):
+            self.ops.copy_(dst, src)
+        else:
+            dst.copy_(src)
+
     def _t(self, *shape, f32=False):
         return torch.zeros(*shape, dtype=torch.float32 if f32 else self.dt, device=self.dev)
 
@@ -727,7 +742,7 @@ class StepEngine:
         ops, g, d, s, B = self.ops, self.g, self.depths, self.s, self.B
         self._side_join("G")
         if z is not g["z"]:
-            g["z"].copy_(z)
+            self._copy(g["z"], z)
         ops.pixnorm(g["z"], g["zn"], self.latent)                            # nets.py:124-125
         Wf = P["latent_format_layer.module.weight"]
         ops.linear(g["zn"], Wf, P["latent_format_layer.module.bias"], g["f"], B=B,
@@ -885,6 +900,8 @@ class StepEngine:
             else:
                 h = D[f"p{i}"]
         self.h_mb = h
+        # the D-buffer key of the mbstd input (the merged second backward needs its 2B view)
+        self.h_mb_key = "yrgb" if s == 0 else ("hblend" if (s == 1 and low) else "p0")
         ops.mbstd_fwd(h, D["m"], B=B, HW=16, C=d[0])                           # blocks.py:261
         self._conv("D", "mb", D["m"], D["c"], 4, d[0] + 1, d[0], L.CONV_LRELU)
         mb = "minibatch_normalization_block.linear.module."
@@ -1151,9 +1168,9 @@ class StepEngine:
         between the real-image part (which does not read G) and the fake image."""
         ops, D, B, hp = self.ops, self.dd, self.B, self.hyper
         GD_flat = self._GD_flat
-        GD_flat.zero_()
-        self.loss[:3].zero_()
-        self.loss[4:5].zero_()
+        self._zero(GD_flat)
+        self._zero(self.loss[:3])
+        self._zero(self.loss[4:5])
         if self._merged():
             return self._d_step_merged(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake, gp_eps)
         if self._low(alpha_D):
@@ -1190,13 +1207,14 @@ class StepEngine:
         return xr, img_fake
 
     def _merged(self):
-        """Whether this D half runs its real and fake passes merged (batch 2B): the R1 mode,
-        2B buffers allocated, no concurrent fake stream, and no generator update still
-        waiting for its DP exchange (that exchange overlaps the real-image part of the
-        separate schedule, which does not read G; the merged forward needs the fake image
-        first)."""
-        return (self.dd2 is not None and self.hyper.gp_mode in ("r1", "wgan-gp") and
-                not hasattr(self._pending_G, "wait"))
+        """Whether this D half runs its real and fake passes merged (batch 2B buffers
+        allocated).  With a generator update still waiting for its DP exchange the R1 mode
+        keeps the second backward merged but runs the two forwards separately, the real
+        image's first (see _d_step_merged_b2); the WGAN-GP mode then keeps the separate
+        schedule."""
+        if self.dd2 is None or self.hyper.gp_mode not in ("r1", "wgan-gp"):
+            return False
+        return self.hyper.gp_mode == "r1" or not hasattr(self._pending_G, "wait")
 
     @contextlib.contextmanager
     def _pair(self):
@@ -1225,6 +1243,8 @@ class StepEngine:
         B = self.B
         D1, D2 = self.dd, self.dd2
         X = D2["xin"]
+        if hasattr(self._pending_G, "wait") and hp.gp_mode == "r1":
+            return self._d_step_merged_b2(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake)
         if before_fake is not None:
             before_fake()
         z_g = self._z_g
@@ -1237,8 +1257,8 @@ class StepEngine:
                 # both generator forwards of the step in one (G is not updated in between):
                 # images [fake for D; fake for G] into X[B:3B], activations kept for the G half
                 g2 = self.g2
-                g2["z"][:B].copy_(z)
-                g2["z"][B:].copy_(z_g)
+                self._copy(g2["z"][:B], z)
+                self._copy(g2["z"][B:], z_g)
                 saved = self.g, self.B
                 self.g, self.B = g2, 2 * B
                 try:
@@ -1250,7 +1270,7 @@ class StepEngine:
             if self._low(alpha_D):
                 ops.img_fade(real, alpha_D, X[:B])                               # :217-221
             else:
-                X[:B].copy_(real)
+                self._copy(X[:B], real)
             with self._pair():
                 self.d_forward(PD, X, alpha_D)                                  # :216, :228
         finally:
@@ -1302,6 +1322,46 @@ class StepEngine:
         self._side_join()
         return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
 
+    def _d_step_merged_b2(self, PG, PD, GD, real, z, alpha_G, alpha_D, before_fake):
+        """The merged R1 D half while the previous step's G gradient is still in its DP
+        exchange (lib/model.py:74-79 is the reference's collective site): the real image's
+        forward, B1, R1 and tangent at batch B first -- none of them reads G, so the exchange
+        completes behind them -- then before_fake (the exchange's wait, Adam_G, the G packing),
+        the generator forward, the fake image's forward at batch B into the second half of
+        the merged buffers, and ONE second backward over [real; fake] at 2B as in
+        _d_step_merged.  Every per-sample quantity is the separate schedule's."""
+        ops = self.ops
+        B = self.B
+        D1, D2 = self.dd, self.dd2
+        X = D2["xin"]
+        if self._low(alpha_D):
+            ops.img_fade(real, alpha_D, X[:B])                                   # :217-221
+        else:
+            self._copy(X[:B], real)
+        self.d_forward(PD, X[:B], alpha_D)                                       # :216
+        ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], D1["hl"])    # lib/loss.py:119-123
+        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1")                     # lib/loss.py:125-135
+        tout, inj = self.d_tangent(PD, GD, gbar, D1["u"], alpha_D)
+        ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
+        if before_fake is not None:
+            before_fake()
+        img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
+        self.dd = self.dd_hi
+        try:
+            self.d_forward(PD, X[B:], alpha_D)                                   # :228
+        finally:
+            self.dd = D1
+        ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u2"][B:], None)
+        self.h_mb = D2[self.h_mb_key]
+        try:
+            with self._pair():
+                # D2["inj"]: the tangent wrote the real half; the fake half stays zero
+                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True)
+        finally:
+            self.h_mb = D1[self.h_mb_key]
+        self._side_join()
+        return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
+
     def _wgan_gp(self, PD, GD, xr, xf, eps, alpha):
         """Optional WGAN-GP mode (pggan/loss.py:54-92): interp -> D -> per-sample grad norm.
         Fused form: the interpolation eps x_r + (1 - eps) x_f is read by the fromRGB layers
@@ -1326,8 +1386,8 @@ class StepEngine:
         """G half of train_step (pggan/model.py:244-253).  before_d() runs after the
         generator forward (which does not read D) and before D is evaluated."""
         ops, D, hp = self.ops, self.dd, self.hyper
-        self._GG_flat.zero_()
-        self.loss[3:4].zero_()
+        self._zero(self._GG_flat)
+        self._zero(self.loss[3:4])
         if self._g_done:
             # the D half ran this half's generator forward (merged): its activations and
             # image are the second half of the 2B generator buffers

@@ -235,8 +235,12 @@ class ProgressiveGAN:
                 self._loader.close()
             if getattr(self, "_aug_gen", None) is None:
                 self._aug_gen = torch.Generator().manual_seed(1000 + self.rank)
+            # decoded images stay in HBM (pggan_amd.data.HbmImageCache): config
+            # hbm_image_cache_gb, default 40 % of the free device memory
+            gb = cfg_get(self.args, "hbm_image_cache_gb", None)
             self._loader = BatchLoader(self.train_dataset, self.device, _lib.HipOps(torch.float32),
-                                       gen=self._aug_gen)
+                                       gen=self._aug_gen,
+                                       cache_bytes=None if gb is None else int(float(gb) * (1 << 30)))
         return self._loader.next(idx, prefetch=self._order[nxt:nxt + B])
 
     def set_loss_collector(self):
@@ -294,19 +298,25 @@ class ProgressiveGAN:
     # ms/step, interleaved A/B in one call, profiles/r3_graph_ab.txt), and the step is
     # GPU-bound (12.5 ms of kernels vs 6.3 ms of host enqueue).
     use_graph = False
+    # the same step recorded once by the library's launch recorder and re-issued from C++
+    # (pg_record_* / pg_replay, world == 1): the host enqueue without the Python layer, on the
+    # engine's own two streams (a hipGraph re-levels them onto other hardware queues)
+    use_replay = False
     graph_replays = 0
 
     def _graph_key(self, eng, B):
         """The key of a replayable step, or None when this step must run eagerly: one
         process, the HIP op set (device-side step counters), no trace hook, packed weights,
         no deferred generator update."""
-        if not (self.use_graph and self._exchange is None and self.device.type == "cuda" and
+        if not ((self.use_graph or self.use_replay) and self._exchange is None and
+                self.device.type == "cuda" and self.hyper.gp_mode == "r1" and
                 hasattr(eng.ops, "randn_dev") and hasattr(eng.ops, "adam_dev") and
                 eng.trace is None and eng.grad_ready is None and not E.FORCE_SERIAL and
                 eng._pending_G is None and all(eng._packed.values())):
             return None
         h = self.hyper
-        return (id(eng), id(self.fpG), id(self.fpD), B, float(self.G.alpha), float(self.D.alpha),
+        return ("replay" if self.use_replay else "graph",
+                id(eng), id(self.fpG), id(self.fpD), B, float(self.G.alpha), float(self.D.alpha),
                 h.lr_G, h.lr_D, h.beta1, h.beta2, h.eps, h.W_adv, h.slope_cfg, h.gp_mode, h.W_gp,
                 h.W_drift)
 
@@ -349,6 +359,27 @@ class ProgressiveGAN:
             gs.clear()
             gs["key"] = key
             return None
+        if key[0] == "replay":
+            if "rec" not in gs:
+                # record the second step while it runs; the recording holds the buffer
+                # pointers of this batch, so later batches are copied into the same buffer
+                gs["real"] = img_real if img_real is self.synthetic else img_real.clone()
+                eng.ops.record_begin()
+                try:
+                    gs["out"] = self._step_body(eng, gs["real"], B)
+                finally:
+                    gs["rec"] = eng.ops.record_end()
+                return gs["out"]
+            if img_real is not gs["real"]:
+                gs["real"].copy_(img_real)
+            self._rng_step += 1
+            self._rng_off_host = self._rng_step * self._z.numel()
+            for fp in (self.fpG, self.fpD):
+                fp.step += 1
+                fp._step_dev_host = fp.step
+            gs["rec"].replay()
+            self.graph_replays += 1
+            return gs["out"]
         if "graph" not in gs:
             gs["real"] = img_real if img_real is self.synthetic else img_real.clone()
             g = torch.cuda.CUDAGraph()

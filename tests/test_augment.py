@@ -167,11 +167,19 @@ def test_batch_loader_end_to_end(tmp_path):
         Image.fromarray(im).save(tmp_path / ("sub" if k % 2 else "") / f"im{k}.png")
     ds = PD.ImageFolderDataset([str(tmp_path)], scale_index=3)      # 32 x 32
     assert len(ds) == 6
-    ld = PD.BatchLoader(ds, "cuda", _lib.HipOps(torch.bfloat16), seed=4, workers=3)
-    got = ld.next([0, 1, 2, 3], prefetch=[4, 5, 0, 1]).cpu().numpy()
-    got2 = ld.next([4, 5, 0, 1]).cpu().numpy()
-    ld.close()
-    g = torch.Generator().manual_seed(4)
-    for idx, out in (([0, 1, 2, 3], got), ([4, 5, 0, 1], got2)):
-        u8 = np.stack([ds.load(i) for i in idx])
-        _assert_bytes_equal(out, A.augment_pil(u8, PD.draw_params(4, g)))
+    batches = [[0, 1, 2, 3], [4, 5, 0, 1], [2, 3, 4, 5], [0, 1, 2, 3]]
+    # cache_bytes: room for 5 of the 6 images (index 5 is decoded every time it comes up),
+    # then no cache; 0: no cache.  Every batch is byte-exact either way.
+    for cache in (5 * 32 * 32 * 3, 0):
+        ld = PD.BatchLoader(ds, "cuda", _lib.HipOps(torch.bfloat16), seed=4, workers=3,
+                            cache_bytes=cache)
+        outs = [ld.next(b, prefetch=batches[(k + 1) % len(batches)]).cpu().numpy()
+                for k, b in enumerate(batches)]
+        decoded = ld.decoded
+        ld.close()
+        # with the cache only the first sight of each image and the uncached index 5 decode
+        assert decoded == (6 + 1 if cache else 16), decoded
+        g = torch.Generator().manual_seed(4)
+        for idx, out in zip(batches, outs):
+            u8 = np.stack([ds.load(i) for i in idx])
+            _assert_bytes_equal(out, A.augment_pil(u8, PD.draw_params(4, g)))

@@ -176,3 +176,85 @@ def _check_g_and_params(tmp_path, r, world, reduce):
             o, c = fp.offsets[n], int(np.prod(fp.shapes[n]))
             d = float((ours[o:o + c] - refp[n].ravel()).abs().max())
             assert d <= 2 * lr + 1e-6, (what, "param", n, d)
+
+
+def _worker_two_steps(rank, world, port, out_dir, reduce_bf16=False):
+    """Two steps of the bucketed exchange, overlapped (the G exchange completes behind the
+    next step's real-image passes: _d_step_merged_b2 on the HIP kernels) and synchronous (the
+    same exchange waited for at once), from the same parameters."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.dirname(here), here, os.path.join(here, "golden")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pggan_amd import _lib
+    from pggan_amd import engine as E
+    from pggan_amd.dp import GradExchange
+    torch.cuda.set_device(0)
+    gsh, dsh = E.g_param_shapes(TINY_DEPTHS, S), E.d_param_shapes(TINY_DEPTHS, S)
+    res = {}
+    for mode in ("overlap", "sync"):
+        PG = {k: torch.from_numpy(v) for k, v in make_params(gsh, seed=811).items()}
+        PD = {k: torch.from_numpy(v) for k, v in make_params(dsh, seed=812).items()}
+        fpG = E.FlatParams(gsh, E.dead_params("G", S), "cuda", PG)
+        fpD = E.FlatParams(dsh, E.dead_params("D", S), "cuda", PD)
+        eng = E.StepEngine(_lib.HipOps(torch.float32), TINY_DEPTHS, S, B, "cuda")
+        eng.bind(fpG, fpD, E.Hyper())
+        ex = GradExchange(world, bucket_bytes=64 << 10,
+                          reduce_dtype=torch.bfloat16 if reduce_bf16 else torch.float32)
+        ex.bind("G", fpG)
+        ex.bind("D", fpD)
+        eng.grad_ready = ex.ready
+
+        def sync_hook(net, g):
+            ex.hook(net, g).wait()
+            return None
+
+        hook = ex.hook if mode == "overlap" else sync_hook
+        merged_b2 = []
+        orig = eng._d_step_merged_b2
+        eng._d_step_merged_b2 = lambda *a, **k: (merged_b2.append(1), orig(*a, **k))[1]
+        for t in range(2):
+            st = make_inputs(B, 4 * 2 ** S, seed=950 + 10 * rank + t)[0]
+            real, z1, z2 = (torch.from_numpy(st[k]).cuda() for k in ("real", "z1", "z2"))
+            eng.train_step(real, z1, z2, 1.0, 1.0, grad_hook=hook)
+            if t == 0:
+                res[mode + "_loss0"] = eng.loss.cpu().numpy().copy()
+        eng.flush()
+        torch.cuda.synchronize()
+        res[mode + "_pD"] = fpD.flat.cpu().numpy()
+        res[mode + "_pG"] = fpG.flat.cpu().numpy()
+        res[mode + "_gD"] = fpD.grad.cpu().numpy()
+        res[mode + "_loss1"] = eng.loss.cpu().numpy()
+        res[mode + "_b2"] = np.array(len(merged_b2))
+        del eng
+    np.savez(os.path.join(out_dir, f"rank{rank}_two.npz"), **res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("reduce", ["f32", "bf16"])
+def test_dp_two_steps_overlapped_vs_synchronous(tmp_path, reduce):
+    """Two DP steps on the HIP kernels with the G exchange overlapped into the next step (its
+    D half runs the real image's passes, then Adam_G and the fake image, then ONE merged
+    second backward: _d_step_merged_b2) against the same exchange waited for at once (the
+    fully merged schedule): the parameters after both steps, the second step's D gradient and
+    losses agree across schedules (fp32 storage: only the summation grid of the batch-B vs
+    batch-2B forwards differs) and are bit-identical across ranks."""
+    world = 2
+    mp.spawn(_worker_two_steps, args=(world, _free_port(), str(tmp_path), reduce == "bf16"),
+             nprocs=world, join=True)
+    r = [np.load(tmp_path / f"rank{i}_two.npz") for i in range(world)]
+    for k in r[0].files:
+        if "loss" not in k:   # the losses are each rank's own shard's
+            assert np.array_equal(r[0][k], r[1][k]), f"{k} differs across ranks"
+    x = r[0]
+    assert int(x["overlap_b2"]) == 1 and int(x["sync_b2"]) == 0, (x["overlap_b2"], x["sync_b2"])
+    for k, tol in (("pD", 1e-6), ("pG", 1e-6), ("gD", 1e-4), ("loss0", 1e-5), ("loss1", 1e-4)):
+        a, b = x["overlap_" + k].astype(np.float64), x["sync_" + k].astype(np.float64)
+        err = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+        assert err <= tol, (k, err)

@@ -21,7 +21,7 @@ def build(args, graph, s):
     ProgressiveGAN.ops_factory = None
     torch.manual_seed(7)
     m = ProgressiveGAN(args, 0)
-    m.use_graph = graph         # (opt-in in the product: PG_GRAPH=1)
+    m.use_graph = graph         # (opt-in in the product: ProgressiveGAN.use_graph)
     m.initialize_models()
     for i in range(1, s + 1):
         m.G.add_block(args.depths[i])
@@ -91,3 +91,56 @@ def test_graph_replay_matches_eager(tmp_path, dtype):
         # near-zero gradient moves one parameter by up to ~2 lr
         dp = float((a["Gp"] - b["Gp"]).abs().max())
         assert dp <= 2 * (step + 1) * graph.hyper.lr_G, (step, dp)
+
+
+def build_replay(args, s):
+    m = build(args, False, s)
+    m.use_replay = True
+    return m
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_cpp_replay_matches_eager_bitwise(tmp_path, dtype):
+    """The step recorded by the library's launch recorder and re-issued from C++ (use_replay,
+    pg_record_* / pg_replay) against the same model stepped eagerly: BITWISE equal after every
+    step -- latents, losses, gradients, parameters, Adam moments -- across an alpha change (a
+    new recording), an external parameter edit (repack, eager step, re-record) and an optimizer
+    state load (the host step count moves alone).  Same kernels on the same streams, and every
+    reduction deterministic, so nothing may differ at all."""
+    args = make_args(tmp_path, depths=list(TINY_DEPTHS), compute_dtype=dtype)
+    s = 3
+    eager, rep = build(args, False, s), build_replay(args, s)
+    for m in (eager, rep):
+        m.G.alpha = m.D.alpha = 0.5
+    replayed = 0
+    # step 0 packs the weights (eager), step 1 is the key's first step (eager), step 2 records
+    # while it runs, 3-5 replay; alpha changes at 6 (eager, 7 records), the parameter edit at 8
+    # and the optimizer load at 10 run eagerly, 11 records again
+    for step in range(12):
+        if step == 6:
+            for m in (eager, rep):
+                m.G.alpha = m.D.alpha = 0.75
+        if step == 8:
+            sd = {k: v.clone() * 1.01 for k, v in eager.G.state_dict().items()}
+            for m in (eager, rep):
+                m.G.load_state_dict(sd)
+        if step == 10:
+            for m in (eager, rep):
+                sd = m.opt_D.state_dict()
+                for st in sd["state"].values():
+                    st["step"] = torch.tensor(float(m.fpD.step - 2))
+                m.opt_D.load_state_dict(sd)
+        n0 = rep.graph_replays
+        eager.train_step()
+        rep.train_step()
+        replayed += rep.graph_replays - n0
+        torch.cuda.synchronize()
+        a, b = state(eager), state(rep)
+        assert eager.fpG.step == rep.fpG.step == step + 1
+        assert int(rep.fpD.step_dev.item()) == rep.fpD.step
+        for k in a:
+            assert torch.equal(a[k], b[k]), (step, k, float((a[k].double() - b[k].double()).abs().max()))
+        assert rep.graph_replays - n0 == (1 if step in (3, 4, 5) else 0), step
+    assert replayed == 3, replayed
+    rec = rep._gstate.get("rec")
+    assert rec is not None and len(rec) > 50, "recording holds the step's launches"

@@ -80,15 +80,17 @@ def test_hip_wgan_gp_step(name, dtype):
     print(K.summarize(rep))
 
 
-@pytest.mark.parametrize("dtype,s,rtol", [(torch.float32, 3, 0.0), (torch.bfloat16, 6, 1e-3)],
+@pytest.mark.parametrize("dtype,s,rtol", [(torch.float32, 3, 1e-6), (torch.bfloat16, 6, 1e-3)],
                          ids=["f32", "bf16"])
 def test_alpha_one_elision_on_hip(dtype, s, rtol):
     """The benchmark runs at alpha = 1 with the exactly-zero fade-in branches elided; the
-    HIP step must equal computing them, over two steps: bitwise in fp32 at tiny widths (the
-    kernels are deterministic, include/pggan_hip.h), and at paper widths at 256^2 in bf16
-    (the bench's fused / sign-bit tiles) within 1e-3 -- there the elided generator backward
-    runs the toRGB input gradient fused with the top PixelNorm backward (fp32 in registers)
-    where the computed branch stores dL/dy in bf16, so the roundings differ."""
+    HIP step must equal computing them, over two steps.  Bitwise on the CPU double
+    (test_engine_cpu); here the two schedules run different kernels where the branch is
+    computed -- the toRGB output with the fade-in term sums its channels in another order
+    (fp32: last-bit differences of the image, 1e-6), the elided generator backward runs the
+    toRGB input gradient fused with the top PixelNorm backward (fp32 in registers) where the
+    computed branch stores dL/dy in bf16 (bf16 at paper widths, 256^2: 1e-3).  Each run is
+    itself bitwise reproducible (test_step_bitwise_reproducible)."""
     from pggan_amd import _lib
     from gen_inputs import TINY_DEPTHS
     from test_engine_cpu import elision_bitwise
