@@ -215,11 +215,14 @@ class KernelTimer:
         return out
 
 
-def pmc_traffic(args, fam):
+def pmc_traffic(args, fam, launches):
     """HBM bytes per launch of `fam` from the newest committed rocprofv3 PMC summary of this
-    same workload (profiles/*_prof_summary.json, written by tools/prof_summary.py from
-    separate --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, gfx950 FETCH x2 correction).
-    PMC counters cannot be read inside the timed run, so this is the profiled twin's value."""
+    same workload AND schedule (profiles/*_prof_summary.json, written by tools/prof_summary.py
+    from separate --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py, gfx950 FETCH x2
+    correction): the summary's call count of the group must equal this run's `launches` per
+    step, so a profile of another schedule (other merges, other tiles) is never paired with
+    the line.  PMC counters cannot be read inside the timed run, so this is the profiled
+    twin's value."""
     import glob
     import re
     key = f"stage{args.stage}_b{args.batch}_{args.dtype}"
@@ -234,7 +237,7 @@ def pmc_traffic(args, fam):
         except (OSError, ValueError):
             continue
         f = d.get("groups", {}).get(fam, {})
-        if d.get("config") == key and f.get("hbm_bytes_per_call"):
+        if d.get("config") == key and f.get("hbm_bytes_per_call") and f.get("calls") == launches:
             return round(f["hbm_bytes_per_call"]), os.path.relpath(p, ROOT)
     return None, None
 
@@ -445,7 +448,7 @@ def main():
                 ach, peak, unit = kd["gbps"], PEAK_HBM_GBS, "GB/s"
             else:
                 ach, peak, unit = kd["tflops"], PEAK_TFLOPS[timer.peak_key(fam)], "TFLOP/s"
-            traffic, tsrc = pmc_traffic(args, dom)
+            traffic, tsrc = pmc_traffic(args, dom, kd["launches"])
             roof = dict(bound=kd["bound"], kernel=dom, achieved=round(ach, 2),
                         peak=peak, unit=unit, frac=round(ach / peak, 4), traffic=traffic,
                         traffic_source=tsrc,

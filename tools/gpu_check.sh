@@ -63,12 +63,6 @@ for step in "$@"; do
            c:1024:16:16:6 c:512:64:32:8 c:512:32:64:22 c:512:32:32:6 c:512:32:32:0 \
            c:256:128:64:8 c:256:64:128:22 c:256:64:64:6 c:128:256:128:8 c:128:128:128:6 \
            c:64:512:256:8 c:64:256:256:6 c:32:512:512:8 c:1024:32:16:7 c:1024:16:32:8 ;;
-    wgsweep)
-      S="w:512:32:64:0 w:256:64:128:0 w:256:64:64:0 w:128:128:256:0 w:128:128:128:0 w:64:256:512:0 w:64:256:256:0 w:32:512:512:0 w:16:512:512:0"
-      for v in 1,2 2,1 4,1; do for tg in 256 512 1024; do
-        echo "== variant $v target $tg" >> gpurun_out/wgsweep.log
-        PG_WG_VARIANT=$v PG_WG_TARGET=$tg timeout -k 10 120 python tools/kbench.py $S >> gpurun_out/wgsweep.log 2>&1 || exit 1
-      done; done; echo "wgsweep done" ;;
     pmcq)   # counters of one kbench spec: PMC_SPEC, PMC_COUNTERS (one pass)
       ROOT=$(pwd); export TMPDIR=/tmp
       ( cd /tmp && timeout -k 10 300 rocprofv3 --pmc ${PMC_COUNTERS} --output-format csv \
@@ -89,12 +83,6 @@ for step in "$@"; do
     opprof) run opprof 300 python tools/op_profile.py --json gpurun_out/opprof.json ;;
     dbg4) run dbg4 600 python tools/debug_buffers.py 4 1.0 ;;
     kloop) run kloop 120 ./tools/kloop_probe ;;   # build: hipcc --offload-arch=gfx950 -O3 -o tools/kloop_probe tools/kloop_probe.hip
-    kgdiag)   # conv_kg with its staging / epilogue switched off or fed contiguously (PG_KG_DIAG)
-      for dg in 0 8 16 24 1 4; do
-        PG_KG=2 PG_KG_DIAG=$dg run kgdiag_$dg 120 python tools/kbench.py --iters 30 c:32:512:512:0 \
-          c:64:256:256:0 c:128:128:128:0 c:256:64:64:0 c:256:128:64:8
-      done ;;
-    kg) run kg 300 python -m pytest tests/test_gpu_ops.py -q -x -k "conv_kg or conv3x3_fwd or sign_bit" ;;
     dp) run dp 600 python -u -m pytest tests/test_gpu_dp.py -x -q --timeout 300 --timeout-method thread ;;
     graph) run graph 600 python -u -m pytest tests/test_gpu_graph.py -x -q --timeout 300 --timeout-method thread ;;
     loader) run loader 600 python tools/loader_bench.py --out gpurun_out/loader.json ;;
