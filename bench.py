@@ -60,9 +60,9 @@ def parse():
     p.add_argument("--no-kernel-events", action="store_true")
     p.add_argument("--graph", action="store_true",
                    help="replay the step as a hipGraph from the second step on (one process)")
-    p.add_argument("--replay", action="store_true",
-                   help="record the step with the library's launch recorder and replay it from "
-                        "C++ from the third step on (one process)")
+    p.add_argument("--eager", action="store_true",
+                   help="enqueue every step from Python (default: the library's C++ replay of "
+                        "the recorded step from the third step on, one process)")
     p.add_argument("--dp-exchange", action="store_true",
                    help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
                         "group), to measure the bookkeeping's cost against the plain step")
@@ -358,9 +358,9 @@ def main():
     # --graph (one process): from the second step on, train_step replays the step captured
     # as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
     model.use_graph = bool(args.graph)
-    # --replay (one process): the step recorded by the library from the second step on and
-    # re-issued from C++ (pg_replay) on the engine's own streams
-    model.use_replay = bool(args.replay) and world == 1 and not args.dp_exchange
+    # the product default (one process): the step recorded by the library and re-issued from
+    # C++ (pg_replay) on the engine's own streams; --eager enqueues every step from Python
+    model.use_replay = not args.eager and not args.graph and world == 1 and not args.dp_exchange
     for _ in range(args.warmup):
         step()
     model.flush()
@@ -513,7 +513,11 @@ def main():
                        "global_batch": B * world, "resolution": R,
                        "parallelism": f"dp{world}"},
             "host_enqueue_ms_per_step": round(host_ms, 3),
-            "graph_replayed_steps": graph_steps,
+            # timed steps re-issued by the library's C++ replay (or a hipGraph with --graph);
+            # the last timed step runs eagerly with the per-launch timers
+            "replayed_steps": graph_steps,
+            "launch_path": ("hipgraph" if args.graph else "eager" if (args.eager or world > 1 or
+                            args.dp_exchange) else "cpp-replay"),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

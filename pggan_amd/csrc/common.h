@@ -157,8 +157,16 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // -> one lane's agent-scope release -> vmcnt(0) -> relaxed agent ticket; the drawer of the last
 // ticket acquires (agent) before reading the partials, and returns the ticket to 0.
 constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
+// per-output-tile tickets of the weight gradients' in-launch slab combine (wgrad_dma_kernel)
+constexpr int PG_SCRATCH_TILE_TICKETS = 4096;
 __host__ __device__ constexpr size_t pg_scratch_floats() {
-  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
+  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS - PG_SCRATCH_TILE_TICKETS;
+}
+__host__ __device__ inline unsigned* pg_scratch_tile_tickets(void* scratch) {
+  return reinterpret_cast<unsigned*>(scratch) + PG_SCRATCH_HDR_FLOATS;
+}
+__host__ __device__ inline float* pg_scratch_partials(float* scratch) {
+  return scratch + PG_SCRATCH_HDR_FLOATS + PG_SCRATCH_TILE_TICKETS;
 }
 
 // Every thread of every workgroup calls this last, uniformly.  tot: LDS, the workgroup's NA
@@ -173,7 +181,7 @@ __device__ __forceinline__ void det_commit(const float* tot, int NA, float* scra
   const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
   const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
-  float* part = scratch + PG_SCRATCH_HDR_FLOATS;
+  float* part = pg_scratch_partials(scratch);
   for (int q = tid; q < NA; q += nt) part[(size_t)bid * NA + q] = tot[q];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -231,7 +239,7 @@ __device__ __forceinline__ void det_commit_seg(float v, int nseg, float* scratch
   const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
   const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
-  float* part = scratch + PG_SCRATCH_HDR_FLOATS;
+  float* part = pg_scratch_partials(scratch);
   if (tid == 0) part[bid] = v;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();

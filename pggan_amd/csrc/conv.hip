@@ -815,6 +815,9 @@ struct WgBParams {
   int gzb_cs;
   float slope;
   int xcd_remap;      // XCD-aware workgroup order (see the kernel prologue)
+  // WG_SLABS with an in-launch combine (wgrad_dma_kernel): one ticket per (o, c) output tile
+  // in the caller's scratch; the last split to arrive sums the tile's slabs in split order
+  unsigned* tickets;
 };
 
 // pixels per staged tile: 128, or 256 (16x16) for the wide tiles at W >= 16 (half the
@@ -1162,16 +1165,18 @@ void wgrad_bf16_kernel(WgBParams p) {
 }
 
 // Sum the split slabs (slab order, deterministic): block x covers 64 consecutive outputs with
-// 4 slab groups (a wave each: 256 contiguous bytes of one slab per load); wave g sums slabs
-// [g*spg, (g+1)*spg) with 4 loads in flight, the 4 group sums are added in group order through
-// LDS and added once to dw / db.  (The former 2-D grid added its y-partials with fp32 atomics:
-// order-dependent results, tools/repro_probe.py.)
-__global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t slab, int splits,
-                                                         int nw, float* dw, float* db, float scale) {
-  __shared__ float part[4][64];
+// G slab groups (a wave each: 256 contiguous bytes of one slab per load); wave g sums slabs
+// [g*spg, (g+1)*spg) with 4 loads in flight, the G group sums are added in group order through
+// LDS and added once to dw / db.  G is picked per shape (wgrad_reduce_groups) so the launch has
+// ~512 x 256 threads in flight like the former 2-D grid, which added its y-partials with fp32
+// atomics (order-dependent results, tools/repro_probe.py).
+template <int G>
+__global__ __launch_bounds__(64 * G) void wgrad_slab_reduce(const float* ws, size_t slab, int splits,
+                                                            int nw, float* dw, float* db, float scale) {
+  __shared__ float part[G][64];
   const int l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const size_t i = (size_t)blockIdx.x * 64 + l;
-  const int spg = (splits + 3) / 4;
+  const int spg = (splits + G - 1) / G;
   const int s0 = g * spg, s1 = min(splits, s0 + spg);
   float s = 0.f;
   if (i < slab) {
@@ -1188,9 +1193,31 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce(const float* ws, size_t
   part[g][l] = s;
   __syncthreads();
   if (g != 0 || i >= slab) return;
-  const float t = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  float t = part[0][l];
+#pragma unroll
+  for (int q = 1; q < G; ++q) t += part[q][l];
   float* dst = i < (size_t)nw ? dw + i : (db ? db + (i - nw) : nullptr);
   if (dst) *dst += t * scale;
+}
+
+// groups per block of wgrad_slab_reduce: enough blocks x groups for ~2048 waves in flight
+static int wgrad_reduce_groups(size_t slab, int splits) {
+  const long nblk = (long)((slab + 63) / 64);
+  int g = 1;
+  while (g < 16 && nblk * g < 2048 && g * 2 <= splits) g *= 2;
+  return g;
+}
+
+static void launch_slab_reduce(const float* ws, size_t slab, int splits, int nw, float* dw, float* db,
+                               float scale, hipStream_t st) {
+  const dim3 grid((unsigned)pg_cdiv((long long)slab, 64));
+  switch (wgrad_reduce_groups(slab, splits)) {
+    case 1: PG_KLAUNCH(wgrad_slab_reduce<1>, grid, dim3(64), 0, st, ws, slab, splits, nw, dw, db, scale); break;
+    case 2: PG_KLAUNCH(wgrad_slab_reduce<2>, grid, dim3(128), 0, st, ws, slab, splits, nw, dw, db, scale); break;
+    case 4: PG_KLAUNCH(wgrad_slab_reduce<4>, grid, dim3(256), 0, st, ws, slab, splits, nw, dw, db, scale); break;
+    case 8: PG_KLAUNCH(wgrad_slab_reduce<8>, grid, dim3(512), 0, st, ws, slab, splits, nw, dw, db, scale); break;
+    default: PG_KLAUNCH(wgrad_slab_reduce<16>, grid, dim3(1024), 0, st, ws, slab, splits, nw, dw, db, scale); break;
+  }
 }
 
 // The same sum, thread = 4 consecutive outputs: one 16-byte load per slab, RSP of them issued
@@ -1298,8 +1325,7 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
     PG_LAUNCH_CHECK();
     return PG_OK;
   }
-  PG_KLAUNCH(wgrad_slab_reduce, dim3((unsigned)pg_cdiv((long long)pl.slab, 64)), dim3(256), 0, st,
-                     ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale);
+  launch_slab_reduce(ws, pl.slab, pl.splits, d->cout * d->cin * 9, dw, db, scale, st);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
@@ -1307,7 +1333,8 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
 // the LDS-DMA weight gradient of the wide layers (wgrad_dma.inc)
 bool wgrad_dma_ok(const pg_conv_desc* d, const WgbPlan& pl);
 int launch_wgrad_dma(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz, float scale,
-                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st, const void* gzbits);
+                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st, const void* gzbits,
+                     void* scratch);
 
 template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false, int BP = WGB_BP>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
@@ -1370,7 +1397,7 @@ constexpr bool wgrad_gzb_ok(int MO, int WNC, int PD, int WPE) {
 
 int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, float scale,
                         float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st,
-                        const void* gzbits = nullptr) {
+                        const void* gzbits, void* scratch) {
   PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS) || gzbits, "wgrad_bf16: GZ_BITS without gzbits");
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
@@ -1379,7 +1406,8 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
     pl.splits = 1;   // no room for the slabs: one split (WG_DIRECT), deterministic
     pl.tiles_per_split = pl.ntiles;
   }
-  if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits);
+  if (wgrad_dma_ok(d, pl))
+    return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits, scratch);
   // (prefetch depth, waves per SIMD) from the round-1 sweep
   const int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   const bool gzb = (d->flags & PG_CONV_GZ_BITS) != 0;
@@ -1820,12 +1848,13 @@ size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d) {
 }
 
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+                     float* dw, float* db, void* ws, size_t ws_bytes, void* scratch, void* stream) {
   PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
   PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS), "conv3x3_wgrad: GZ_BITS needs pg_conv3x3_wgrad_ex");
   if (dtype == PG_BF16)
-    return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream);
+    return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream,
+                               nullptr, scratch);
   TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
   WgParams p;
   p.x = x; p.gz = gz; p.dw = dw; p.db = db;
@@ -1857,22 +1886,21 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
   else
     PG_KLAUNCH(wgrad3x3_kernel<bf16_t>, grid, dim3(256), lds, st, p);
   if (p.ws)
-    PG_KLAUNCH(wgrad_slab_reduce, dim3((unsigned)pg_cdiv((long long)p.slab, 64)), dim3(256), 0, st,
-                       p.ws, p.slab, splits, d->cout * d->cin * 9, dw, db, scale);
+    launch_slab_reduce(p.ws, p.slab, splits, d->cout * d->cin * 9, dw, db, scale, st);
   PG_LAUNCH_CHECK();
   return PG_OK;
 }
 
 int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const void* gz,
                         const void* gzbits, float scale, float* dw, float* db, void* ws,
-                        size_t ws_bytes, void* stream) {
+                        size_t ws_bytes, void* scratch, void* stream) {
   if (!d || !(d->flags & PG_CONV_GZ_BITS))
-    return pg_conv3x3_wgrad(dtype, d, x, gz, scale, dw, db, ws, ws_bytes, stream);
+    return pg_conv3x3_wgrad(dtype, d, x, gz, scale, dw, db, ws, ws_bytes, scratch, stream);
   PG_CHECK_ARG(x && gz && gzbits && dw && dtype == PG_BF16, "conv3x3_wgrad_ex: GZ_BITS needs gzbits (bf16)");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4 && d->H % 2 == 0 && d->W % 2 == 0,
                "conv3x3_wgrad_ex: bad spatial size");
   return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream,
-                             gzbits);
+                             gzbits, scratch);
 }
 
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,

@@ -299,9 +299,13 @@ class ProgressiveGAN:
     # GPU-bound (12.5 ms of kernels vs 6.3 ms of host enqueue).
     use_graph = False
     # the same step recorded once by the library's launch recorder and re-issued from C++
-    # (pg_record_* / pg_replay, world == 1): the host enqueue without the Python layer, on the
-    # engine's own two streams (a hipGraph re-levels them onto other hardware queues)
-    use_replay = False
+    # (pg_record_* / pg_replay, world == 1, R1 mode): the host enqueue without the Python layer
+    # (1.5 vs 4.6 ms per C5 step), on the engine's own two streams (a hipGraph re-levels them
+    # onto other hardware queues).  Bitwise the eager step (tests/test_gpu_graph.py).  The
+    # first step of a (stage, batch, alpha, hyper-parameter) key runs eagerly, the second is
+    # recorded while it runs, later ones replay; anything the key does not see -- a parameter
+    # edited through .data, a buffer reallocated -- needs _params_changed() or use_replay off.
+    use_replay = True
     graph_replays = 0
 
     def _graph_key(self, eng, B):

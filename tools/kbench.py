@@ -54,8 +54,10 @@ def run(ops, spec, B, iters):
         byts = sum(t.numel() * t.element_size() for t in (x, y, aux, y2, xbits) if t is not None)
     else:
         # w flags: 1 = UPS_IN (x at half resolution), 2 = GZ_BITS (g at half resolution,
-        # masked by lrelu' sign bits at full resolution: the D conv-b weight gradient)
-        ups, gzb = bool(fl & 1), bool(fl & 2)
+        # masked by lrelu' sign bits at full resolution: the D conv-b weight gradient),
+        # 4 = the split slabs summed by the separate reduction launch (A/B against the
+        # default in-launch combine)
+        ups, gzb, rl = bool(fl & 1), bool(fl & 2), bool(fl & 4)
         Hin = H // 2 if ups else H
         x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
         Hg = H // 2 if gzb else H
@@ -65,14 +67,14 @@ def run(ops, spec, B, iters):
         dw = torch.zeros(cout, cin, 3, 3, device=dev)
         db = torch.zeros(cout, device=dev)
 
-        # the split-partial workspace the engine passes (WG_SLABS + the reduction launch);
-        # without one the kernel would fall back to fp32 atomics
+        # the split-partial workspace the engine passes (WG_SLABS); without one the plan
+        # falls back to one split
         nbw = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=ups)
         wsw = torch.empty(max(nbw // 4, 1), device=dev) if nbw else None
 
         def f():
             ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=1.0,
-                           db=db, ws=wsw, gzbits=bits)
+                           db=db, ws=wsw, gzbits=bits, reduce_launch=rl)
         byts = x.numel() * 2 + gz.numel() * 2 + (bits.numel() if gzb else 0)
     for _ in range(3):
         f()
