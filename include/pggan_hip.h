@@ -93,11 +93,6 @@ size_t pg_scratch_bytes(void);
  * gradient through an upsampling conv a, then the previous block's PixelNorm).  Not with
  * BIAS / MASK / ACCUM / PIXNORM / bit flags. */
 #define PG_CONV_PNBWD 2048
-/* weight gradient with split slabs (ws): by default the wide LDS-DMA kernel combines up to 16
- * splits inside the launch -- the last split of each output tile to finish sums the tile's
- * slabs in split order, with a ticket in `scratch` (NULL scratch: the separate launch); this
- * flag forces the separate reduction launch (A/B runs).  Both are deterministic. */
-#define PG_CONV_WG_REDUCE_LAUNCH 4096
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -153,12 +148,12 @@ int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);
  * second kernel adds them into dw/db; NULL or too small -> fp32 atomics per split. */
 size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d);
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, float* db, void* ws, size_t ws_bytes, void* scratch, void* stream);
+                     float* dw, float* db, void* ws, size_t ws_bytes, void* stream);
 /* pg_conv3x3_wgrad with PG_CONV_GZ_BITS: gz at half resolution (channel stride y_cs),
  * gzbits at full resolution (xb_cs bytes per pixel); bf16 only */
 int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const void* gz,
                         const void* gzbits, float scale, float* dw, float* db, void* ws,
-                        size_t ws_bytes, void* scratch, void* stream);
+                        size_t ws_bytes, void* stream);
 /* bias gradient, accumulates: db[c] += scale * sum_p g[p][c] */
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,
                  void* scratch, void* stream);

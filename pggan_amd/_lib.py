@@ -19,7 +19,6 @@ CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 
 CONV_PIXNORM = 64
 CONV_PNBWD = 2048
 CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
-CONV_WG_REDUCE_LAUNCH = 4096
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
     1, 2, 4, 8, 16, 32, 64)
@@ -100,10 +99,10 @@ _SIGS = {
     "pg_conv3x3_fwd_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                            _SZ, _VP], _I),
     "pg_conv3x3_wgrad_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _F, _VP, _VP, _VP, _SZ,
-                             _VP, _VP], _I),
+                             _VP], _I),
     "pg_conv3x3_wgrad_workspace_size": ([_I, ctypes.POINTER(ConvDesc)], _SZ),
-    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP,
-                          _VP], _I),
+    "pg_conv3x3_wgrad": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _F, _VP, _VP, _VP, _SZ, _VP],
+                         _I),
     "pg_bias_grad": ([_I, _I, _I, _I, _VP, _F, _VP, _VP, _VP], _I),
     "pg_pixnorm_fwd": ([_I, _I, _I, _I, _VP, _VP, _VP], _I),
     "pg_pixnorm_lrelu_bwd": ([_I, _I, _I, _I, _VP, _VP, _F, _I, _VP, _VP], _I),
@@ -422,20 +421,17 @@ class HipOps:
         return int(self.lib.pg_conv3x3_wgrad_workspace_size(self.dt, ctypes.byref(d)))
 
     def conv_wgrad(self, x, gz, dw, *, B, H, W, cin, cout, ups, scale, db=None, ws=None,
-                   gzbits=None, slope=0.2, reduce_launch=False):
+                   gzbits=None, slope=0.2):
         """ws: optional fp32 workspace (see wgrad_workspace_bytes) for split reductions.
-        gzbits: the gradient is up2(gz) * lrelu'(gzbits) (gz at H/2, bits uint8 at H).
-        reduce_launch: sum the split slabs in a separate launch instead of in the launch
-        (PG_CONV_WG_REDUCE_LAUNCH, A/B runs)."""
+        gzbits: the gradient is up2(gz) * lrelu'(gzbits) (gz at H/2, bits uint8 at H)."""
         self._cuda(x, gz, dw, db, ws, gzbits)
-        fl = (CONV_UPS_IN if ups else 0) | (CONV_GZ_BITS if gzbits is not None else 0) | \
-            (CONV_WG_REDUCE_LAUNCH if reduce_launch else 0)
+        fl = (CONV_UPS_IN if ups else 0) | (CONV_GZ_BITS if gzbits is not None else 0)
         d = ConvDesc(B, H, W, cin, cout, x.shape[-1], gz.shape[-1], 0, 0, fl, slope, 1.0,
                      gzbits.shape[-1] if gzbits is not None else 0)
         wsb = ws.numel() * ws.element_size() if ws is not None else 0
         self._chk(self.lib.pg_conv3x3_wgrad_ex(self._dt(gz), ctypes.byref(d), _p(x), _p(gz),
                                                _p(gzbits), scale, _p(dw), _p(db), _p(ws), wsb,
-                                               self._scr(), self._s()),
+                                               self._s()),
                   "conv3x3_wgrad")
 
     def bias_grad(self, g, db, C, scale):

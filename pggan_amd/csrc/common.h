@@ -157,16 +157,11 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // -> one lane's agent-scope release -> vmcnt(0) -> relaxed agent ticket; the drawer of the last
 // ticket acquires (agent) before reading the partials, and returns the ticket to 0.
 constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
-// per-output-tile tickets of the weight gradients' in-launch slab combine (wgrad_dma_kernel)
-constexpr int PG_SCRATCH_TILE_TICKETS = 4096;
 __host__ __device__ constexpr size_t pg_scratch_floats() {
-  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS - PG_SCRATCH_TILE_TICKETS;
-}
-__host__ __device__ inline unsigned* pg_scratch_tile_tickets(void* scratch) {
-  return reinterpret_cast<unsigned*>(scratch) + PG_SCRATCH_HDR_FLOATS;
+  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
 }
 __host__ __device__ inline float* pg_scratch_partials(float* scratch) {
-  return scratch + PG_SCRATCH_HDR_FLOATS + PG_SCRATCH_TILE_TICKETS;
+  return scratch + PG_SCRATCH_HDR_FLOATS;
 }
 
 // Every thread of every workgroup calls this last, uniformly.  tot: LDS, the workgroup's NA

@@ -815,9 +815,6 @@ struct WgBParams {
   int gzb_cs;
   float slope;
   int xcd_remap;      // XCD-aware workgroup order (see the kernel prologue)
-  // WG_SLABS with an in-launch combine (wgrad_dma_kernel): one ticket per (o, c) output tile
-  // in the caller's scratch; the last split to arrive sums the tile's slabs in split order
-  unsigned* tickets;
 };
 
 // pixels per staged tile: 128, or 256 (16x16) for the wide tiles at W >= 16 (half the
@@ -1333,8 +1330,7 @@ int wgrad_slab_finish(const pg_conv_desc* d, const WgbPlan& pl, int mode, const 
 // the LDS-DMA weight gradient of the wide layers (wgrad_dma.inc)
 bool wgrad_dma_ok(const pg_conv_desc* d, const WgbPlan& pl);
 int launch_wgrad_dma(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz, float scale,
-                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st, const void* gzbits,
-                     void* scratch);
+                     float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st, const void* gzbits);
 
 template <int MO, int NC, int WMO, int WNC, int PD, int WPE, bool GZB = false, int BP = WGB_BP>
 int launch_wgrad_bf16(const pg_conv_desc* d, const WgbPlan& pl, const void* x, const void* gz,
@@ -1397,7 +1393,7 @@ constexpr bool wgrad_gzb_ok(int MO, int WNC, int PD, int WPE) {
 
 int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, float scale,
                         float* dw, float* db, float* ws, size_t ws_bytes, hipStream_t st,
-                        const void* gzbits, void* scratch) {
+                        const void* gzbits = nullptr) {
   PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS) || gzbits, "wgrad_bf16: GZ_BITS without gzbits");
   PG_CHECK_ARG(d->cout % 8 == 0 && d->x_cs % 8 == 0 && d->y_cs % 8 == 0,
                "wgrad_bf16: cout (%d) and channel strides must be multiples of 8", d->cout);
@@ -1406,8 +1402,7 @@ int wgrad_bf16_dispatch(const pg_conv_desc* d, const void* x, const void* gz, fl
     pl.splits = 1;   // no room for the slabs: one split (WG_DIRECT), deterministic
     pl.tiles_per_split = pl.ntiles;
   }
-  if (wgrad_dma_ok(d, pl))
-    return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits, scratch);
+  if (wgrad_dma_ok(d, pl)) return launch_wgrad_dma(d, pl, x, gz, scale, dw, db, ws, ws_bytes, st, gzbits);
   // (prefetch depth, waves per SIMD) from the round-1 sweep
   const int pd = pl.MO >= 4 ? 4 : 2, wpe = pl.MO >= 4 ? 1 : (pl.MO * pl.WNC >= 2 ? 2 : 3);
   const bool gzb = (d->flags & PG_CONV_GZ_BITS) != 0;
@@ -1848,13 +1843,12 @@ size_t pg_conv3x3_wgrad_workspace_size(int dtype, const pg_conv_desc* d) {
 }
 
 int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void* gz, float scale,
-                     float* dw, float* db, void* ws, size_t ws_bytes, void* scratch, void* stream) {
+                     float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   PG_CHECK_ARG(d && x && gz && dw, "conv3x3_wgrad: null pointer");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4, "conv3x3_wgrad: bad spatial size");
   PG_CHECK_ARG(!(d->flags & PG_CONV_GZ_BITS), "conv3x3_wgrad: GZ_BITS needs pg_conv3x3_wgrad_ex");
   if (dtype == PG_BF16)
-    return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream,
-                               nullptr, scratch);
+    return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream);
   TileCfg tc = pick_tile(d->H, d->W, WG_BP, 32);
   WgParams p;
   p.x = x; p.gz = gz; p.dw = dw; p.db = db;
@@ -1893,14 +1887,14 @@ int pg_conv3x3_wgrad(int dtype, const pg_conv_desc* d, const void* x, const void
 
 int pg_conv3x3_wgrad_ex(int dtype, const pg_conv_desc* d, const void* x, const void* gz,
                         const void* gzbits, float scale, float* dw, float* db, void* ws,
-                        size_t ws_bytes, void* scratch, void* stream) {
+                        size_t ws_bytes, void* stream) {
   if (!d || !(d->flags & PG_CONV_GZ_BITS))
-    return pg_conv3x3_wgrad(dtype, d, x, gz, scale, dw, db, ws, ws_bytes, scratch, stream);
+    return pg_conv3x3_wgrad(dtype, d, x, gz, scale, dw, db, ws, ws_bytes, stream);
   PG_CHECK_ARG(x && gz && gzbits && dw && dtype == PG_BF16, "conv3x3_wgrad_ex: GZ_BITS needs gzbits (bf16)");
   PG_CHECK_ARG(d->B > 0 && d->H >= 4 && d->W >= 4 && d->H % 2 == 0 && d->W % 2 == 0,
                "conv3x3_wgrad_ex: bad spatial size");
   return wgrad_bf16_dispatch(d, x, gz, scale, dw, db, (float*)ws, ws_bytes, (hipStream_t)stream,
-                             gzbits, scratch);
+                             gzbits);
 }
 
 int pg_bias_grad(int dtype, int npix, int C, int cs, const void* g, float scale, float* db,

@@ -188,7 +188,6 @@ ENGINE_DEFAULTS = dict(
     dbits_min_res=512,     # ... from this resolution; below it the unpool-pass bits (_ubits)
     fuse_ubits=True,
     fuse_rgbbits=True,     # the top fromRGB output's sign bits (see _rgbbits)
-    wgrad_reduce_launch=False,  # split slabs summed in the wgrad launch (False) or a 2nd launch
 )
 
 
@@ -552,8 +551,6 @@ class StepEngine:
         gscale * up2(g) * lrelu'(gzbits) (never materialised)."""
         c = self.packs[(net, key)][3]
         kw = dict(gzbits=gzbits, slope=SLOPE) if gzbits is not None else {}
-        if self.wgrad_reduce_launch:
-            kw["reduce_launch"] = True
         if self.side is None or FORCE_SERIAL:
             need = self._ws_need("w", H, cin, cout, ups)
             self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,

@@ -155,17 +155,13 @@ WGRAD_CASES = [(2, 8, 32, 48, False), (2, 16, 16, 16, True), (4, 4, 513, 512, Fa
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("use_ws", [True, "launch", False])
+@pytest.mark.parametrize("use_ws", [True, False])
 @pytest.mark.parametrize("case", WGRAD_CASES)
 def test_conv3x3_wgrad(case, dtype, use_ws):
-    """Weight + fused bias gradient.  With a workspace the pixel splits write fp32 slabs,
-    summed in split order inside the launch (the wide LDS-DMA kernel, <= 16 splits: the last
-    split of each output tile to finish) or by the reduction launch ("launch":
-    PG_CONV_WG_REDUCE_LAUNCH, and every other kernel); without one the plan runs one split.
-    Every form is deterministic."""
+    """Weight + fused bias gradient.  With a workspace the pixel splits write fp32 slabs
+    summed in split order by the reduction launch; without one the plan runs one split.  Both
+    are deterministic."""
     B, H, cin, cout, ups = case
-    if dtype == torch.float32 and use_ws == "launch":
-        pytest.skip("the f32 kernel always reduces in a separate launch")
     hip, cpu = ops_pair(dtype)
     Hin = H // 2 if ups else H
     x = q(rnd(B, Hin, Hin, cinp(cin), seed=11), dtype)
@@ -179,9 +175,8 @@ def test_conv3x3_wgrad(case, dtype, use_ws):
         if use_ws and dev == "cuda":
             nb = ops.wgrad_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout, ups=ups)
             ws = torch.full((max(nb // 4, 1),), float("nan"), device=dev)
-        kw = dict(reduce_launch=use_ws == "launch") if dev == "cuda" else {}
         ops.conv_wgrad(x.to(dev).to(dt), gz.to(dev).to(dt), dw, B=B, H=H, W=H, cin=cin, cout=cout,
-                       ups=ups, scale=0.3, db=db, ws=ws, **kw)
+                       ups=ups, scale=0.3, db=db, ws=ws)
         outs.append((dw, db))
     tol = 2e-5 if dtype == torch.float32 else 1e-4
     cmp(outs[0][0], outs[1][0], tol, "wgrad")

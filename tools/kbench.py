@@ -54,10 +54,8 @@ def run(ops, spec, B, iters):
         byts = sum(t.numel() * t.element_size() for t in (x, y, aux, y2, xbits) if t is not None)
     else:
         # w flags: 1 = UPS_IN (x at half resolution), 2 = GZ_BITS (g at half resolution,
-        # masked by lrelu' sign bits at full resolution: the D conv-b weight gradient),
-        # 4 = the split slabs summed by the separate reduction launch (A/B against the
-        # default in-launch combine)
-        ups, gzb, rl = bool(fl & 1), bool(fl & 2), bool(fl & 4)
+        # masked by lrelu' sign bits at full resolution: the D conv-b weight gradient)
+        ups, gzb = bool(fl & 1), bool(fl & 2)
         Hin = H // 2 if ups else H
         x = torch.randn(B, Hin, Hin, cp, device=dev, generator=g).to(bf)
         Hg = H // 2 if gzb else H
@@ -74,7 +72,7 @@ def run(ops, spec, B, iters):
 
         def f():
             ops.conv_wgrad(x, gz, dw, B=B, H=H, W=H, cin=cin, cout=cout, ups=ups, scale=1.0,
-                           db=db, ws=wsw, gzbits=bits, reduce_launch=rl)
+                           db=db, ws=wsw, gzbits=bits)
         byts = x.numel() * 2 + gz.numel() * 2 + (bits.numel() if gzb else 0)
     for _ in range(3):
         f()
