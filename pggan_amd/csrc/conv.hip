@@ -1557,7 +1557,10 @@ int conv_splits(const pg_conv_desc* d) {
   const int base = pg_cdiv(d->B, tc.NB) * (d->W / tc.TW) * (d->H / tc.TH) * pg_cdiv(cout_p, BN);
   const int cin_p = cinp_of(d->cin);
   const int nch = cin_p / (cin_p < 32 ? cin_p : 32);
-  constexpr int min_base = 128, target = 256;   // round-2 split sweep
+  // round-2 split sweep; round 5: min_base 128 -> 256 splits the 16^2 512 -> 512 convs of the
+  // merged passes (B = 8: 128 tiles) in two, 31.2 -> 27.1 us per launch with the epilogue
+  // (profiles/r5_lowres_tiles.txt)
+  constexpr int min_base = 256, target = 256;
   if (base >= min_base || nch < 4) return 1;
   int sp = pg_cdiv(target, base);
   if (sp > nch) sp = nch;
