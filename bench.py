@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--dp-exchange", action="store_true",
                    help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
                         "group), to measure the bookkeeping's cost against the plain step")
+    p.add_argument("--dp-bucket-mb", type=float, default=32.0,
+                   help="DP all-reduce bucket size (config dp_bucket_mb)")
     return p.parse_args()
 
 
@@ -292,7 +294,8 @@ def build_model(args, rank, local, world, ops_factory):
     cfg.update(depths=list(PAPER_DEPTHS), batch_per_gpu=args.batch, compute_dtype=args.dtype,
                synthetic_data=True, isMaster=False, use_mGPU=world > 1, gpu_num=world,
                run_id="bench", gp_mode=args.gp_mode,
-               dp_exchange_world1=bool(args.dp_exchange and world == 1))
+               dp_exchange_world1=bool(args.dp_exchange and world == 1),
+               dp_bucket_mb=args.dp_bucket_mb)
     ProgressiveGAN.ops_factory = ops_factory
     torch.manual_seed(1234)                      # same init on every rank (then broadcast)
     m = ProgressiveGAN(cfg, local)
@@ -358,9 +361,10 @@ def main():
     # --graph (one process): from the second step on, train_step replays the step captured
     # as a hipGraph (ProgressiveGAN.use_graph); off by default (slower on the GPU)
     model.use_graph = bool(args.graph)
-    # the product default (one process): the step recorded by the library and re-issued from
-    # C++ (pg_replay) on the engine's own streams; --eager enqueues every step from Python
-    model.use_replay = not args.eager and not args.graph and world == 1 and not args.dp_exchange
+    # the product default: the step recorded by the library and re-issued from C++ (pg_replay)
+    # on the engine's own streams, under DP with the exchange's collectives and waits recorded
+    # between the launch segments; --eager enqueues every step from Python
+    model.use_replay = not args.eager and not args.graph
     for _ in range(args.warmup):
         step()
     model.flush()
@@ -516,8 +520,8 @@ def main():
             # timed steps re-issued by the library's C++ replay (or a hipGraph with --graph);
             # the last timed step runs eagerly with the per-launch timers
             "replayed_steps": graph_steps,
-            "launch_path": ("hipgraph" if args.graph else "eager" if (args.eager or world > 1 or
-                            args.dp_exchange) else "cpp-replay"),
+            "launch_path": ("hipgraph" if args.graph else "eager" if args.eager else
+                            "cpp-replay"),
             "roofline": roof,
             "cpu_baseline": cpu,
         }

@@ -15,16 +15,41 @@ step, in buckets launched as the final backward pass finishes each layer:
   step's real-image D part for G; engine.train_step).
 
 A collective enqueued on the RCCL stream waits for the compute stream at the time of
-the call, so every bucket sees its finished gradient.  `reduce_dtype=torch.bfloat16`
+the call, so every bucket sees its finished gradient.
+
+Every host action of the exchange (a bucket's all-reduce, sealing a net's exchange into its
+Pending, the wait before Adam) goes through `_act`: while `ProgressiveGAN` records a step for
+the C++ replay (`record_hook` set), the action is also appended to the recording between the
+library's launch segments, so a replayed step issues the same collectives and waits at the
+same points of the launch sequence, on the same streams.  `reduce_dtype=torch.bfloat16`
 halves the bytes on the links (gradients rounded to bf16 before the sum: an opt-in
 trade, the default fp32 keeps the DP contract exact to fp32 rounding).
 """
 from __future__ import annotations
 
+import functools
 import time
 
 import torch
 import torch.distributed as dist
+
+
+def _stream_of(t):
+    """The current stream of a CUDA tensor's device (None for CPU tensors)."""
+    return torch.cuda.current_stream(t.device) if t.is_cuda else None
+
+
+class Handle:
+    """What `finish` returns to the engine (its grad_hook result): wait() completes the
+    net's exchange.  The exchange itself lives in GradExchange._pending, so a replayed step's
+    sealed exchange is the one the next wait finds."""
+
+    def __init__(self, ex, net):
+        self.ex, self.net = ex, net
+
+    def wait(self):
+        self.ex._act(functools.partial(self.ex._wait_now, self.net,
+                                       _stream_of(self.ex._fp[self.net].grad)))
 
 
 class Pending:
@@ -59,6 +84,9 @@ class GradExchange:
         self.group = group
         self._fp = {}
         self._state = {}
+        self._pending = {}     # net -> the sealed, in-flight exchange (Pending)
+        # set while a step is recorded for replay: called with each host action
+        self.record_hook = None
         self.calls = 0          # collectives launched, and the host seconds spent in them
         self.host_s = 0.0
         # set by the engine around ready(): called once before ready() launches a collective
@@ -70,18 +98,48 @@ class GradExchange:
         self._fp[net] = fp
         self._state[net] = dict(works=[], casts=[], pend=[], pend_elems=0, sent=[])
 
+    def _act(self, fn):
+        """Run one host action now (and append it to a step being recorded)."""
+        if self.record_hook is not None:
+            self.record_hook(fn)
+        fn()
+
     def _launch(self, net, lo, hi):
+        self._state[net]["sent"].append((lo, hi))
+        self._act(functools.partial(self._launch_now, net, lo, hi, _stream_of(self._fp[net].grad)))
+
+    def _launch_now(self, net, lo, hi, stream):
         t0 = time.perf_counter()
         st, g = self._state[net], self._fp[net].grad
-        st["sent"].append((lo, hi))
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                self._all_reduce(st, g, lo, hi)
+        else:
+            self._all_reduce(st, g, lo, hi)
+        self.calls += 1
+        self.host_s += time.perf_counter() - t0
+
+    def _all_reduce(self, st, g, lo, hi):
         if self.reduce_dtype == torch.float32:
             st["works"].append(dist.all_reduce(g[lo:hi], group=self.group, async_op=True))
         else:
             buf = g[lo:hi].to(self.reduce_dtype)
             st["works"].append(dist.all_reduce(buf, group=self.group, async_op=True))
             st["casts"].append((lo, hi, buf))
-        self.calls += 1
-        self.host_s += time.perf_counter() - t0
+
+    def _seal(self, net):
+        """The collectives launched for `net` since the last seal become its Pending."""
+        st = self._state[net]
+        self._pending[net] = Pending(st["works"], self._fp[net].grad, self.world, st["casts"])
+        st["works"], st["casts"] = [], []
+
+    def _wait_now(self, net, stream):
+        p = self._pending.pop(net)
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                p.wait()
+        else:
+            p.wait()
 
     def _launch_merged(self, net, ranges):
         """One collective per maximal contiguous span of `ranges`."""
@@ -126,9 +184,9 @@ class GradExchange:
         if pos < fp.n_live:
             rest.append((pos, fp.n_live))
         self._launch_merged(net, rest)
-        p = Pending(st["works"], fp.grad, self.world, st["casts"])
-        self.bind(net, fp)
-        return p
+        self._act(functools.partial(self._seal, net))
+        st["pend"], st["pend_elems"], st["sent"] = [], 0, []
+        return Handle(self, net)
 
     def hook(self, net, g):
         """engine.train_step grad_hook."""

@@ -188,6 +188,7 @@ ENGINE_DEFAULTS = dict(
     dbits_min_res=512,     # ... from this resolution; below it the unpool-pass bits (_ubits)
     fuse_ubits=True,
     fuse_rgbbits=True,     # the top fromRGB output's sign bits (see _rgbbits)
+    overlap_g_exchange=True,  # DP: the G all-reduce behind the next step's real-image part
 )
 
 
@@ -1247,26 +1248,9 @@ class StepEngine:
             return self._d_step_merged_b2(PG, PD, GD, real, z, alpha_G, alpha_D, before_fake)
         if before_fake is not None:
             before_fake()
-        z_g = self._z_g
-        self._z_g = None
-        if z_g is None:
-            img_fake = self.g_forward(PG, z, alpha_G, keep=False)               # :226-227
+        img_fake = self._g_forward_d_half(PG, z, alpha_G)                       # :226-227
         trace, self.trace = self.trace, None
         try:
-            if z_g is not None:
-                # both generator forwards of the step in one (G is not updated in between):
-                # images [fake for D; fake for G] into X[B:3B], activations kept for the G half
-                g2 = self.g2
-                self._copy(g2["z"][:B], z)
-                self._copy(g2["z"][B:], z_g)
-                saved = self.g, self.B
-                self.g, self.B = g2, 2 * B
-                try:
-                    self.g_forward(PG, g2["z"], alpha_G, keep=True)             # :226-227, :244-245
-                finally:
-                    self.g, self.B = saved
-                self._g_done = True
-                img_fake = self.g["img"]
             if self._low(alpha_D):
                 ops.img_fade(real, alpha_D, X[:B])                               # :217-221
             else:
@@ -1275,13 +1259,6 @@ class StepEngine:
                 self.d_forward(PD, X, alpha_D)                                  # :216, :228
         finally:
             self.trace = trace
-        if trace is not None and z_g is not None:
-            trace("G", self)            # the D half's generator forward, then the G half's
-            self.g = self.g_hi
-            try:
-                trace("G", self)
-            finally:
-                self.g = self.g_lo
         h2 = self.h_mb
         self.h_mb = h2[:B]
         if trace is not None:   # one record per image, in the separate schedule's order
@@ -1322,6 +1299,37 @@ class StepEngine:
         self._side_join()
         return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
 
+    def _g_forward_d_half(self, PG, z, alpha_G):
+        """The D half's generator forward (the fake image).  With a merged generator forward
+        pending (self._z_g, see train_step) both generator forwards of the step run as one
+        (G is not updated in between): latents [z; z_g], images [fake for D; fake for G] into
+        the merged input's X[B:3B], activations kept for the G half (its g_step then skips
+        its own forward)."""
+        z_g = self._z_g
+        self._z_g = None
+        if z_g is None:
+            return self.g_forward(PG, z, alpha_G, keep=False)                 # :226-227
+        B, g2 = self.B, self.g2
+        self._copy(g2["z"][:B], z)
+        self._copy(g2["z"][B:], z_g)
+        trace, self.trace = self.trace, None
+        saved = self.g, self.B
+        self.g, self.B = g2, 2 * B
+        try:
+            self.g_forward(PG, g2["z"], alpha_G, keep=True)                     # :226-227, :244-245
+        finally:
+            self.g, self.B = saved
+            self.trace = trace
+        self._g_done = True
+        if trace is not None:
+            trace("G", self)            # the D half's generator forward, then the G half's
+            self.g = self.g_hi
+            try:
+                trace("G", self)
+            finally:
+                self.g = self.g_lo
+        return self.g["img"]
+
     def _d_step_merged_b2(self, PG, PD, GD, real, z, alpha_G, alpha_D, before_fake):
         """The merged R1 D half while the previous step's G gradient is still in its DP
         exchange (lib/model.py:74-79 is the reference's collective site): the real image's
@@ -1345,7 +1353,7 @@ class StepEngine:
         ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
         if before_fake is not None:
             before_fake()
-        img_fake = self.g_forward(PG, z, alpha_G, keep=False)                   # :226-227
+        img_fake = self._g_forward_d_half(PG, z, alpha_G)                       # :226-227
         self.dd = self.dd_hi
         try:
             self.d_forward(PD, X[B:], alpha_D)                                   # :228
@@ -1459,13 +1467,18 @@ class StepEngine:
         The arithmetic and its order per parameter are the reference's either way."""
         fpG, fpD, hp = self.fpG, self.fpD, self.hyper
         PG, PD = fpG.views, fpD.views
+        if not self.overlap_g_exchange:
+            self._finish_G()   # the previous step's G exchange completes first (no B2 reorder)
         if self._pending_G is None and not self._packed["G"]:
             self.pack("G", PG)
         if not self._packed["D"]:
             self.pack("D", PD)
-        # z2 for a merged generator forward (_d_step_merged): not with a bucketed DP exchange
-        # (grad_ready set), whose D all-reduce the G half's own generator forward hides
-        self._z_g = z2 if (self.g2 is not None and self.grad_ready is None) else None
+        # z2 for a merged generator forward (_d_step_merged).  Also under a bucketed DP
+        # exchange: the D gradients go out layer by layer during the last backward (the
+        # 512-channel bulk first), so at its end only the last bucket is in flight, and the
+        # separate G-half generator forward that would hide it costs more than it hides
+        # (one rank, interleaved: profiles/r5_dp_ab.txt)
+        self._z_g = z2 if self.g2 is not None else None
         img_real, img_fake_D = self.d_step(PG, PD, fpD.gviews, real, z1, alpha_G, alpha_D,
                                            gp_eps=gp_eps, before_fake=self._finish_G)
         if self._z_g is not None:   # d_step did not merge: the G half runs its own forward

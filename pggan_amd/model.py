@@ -24,6 +24,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import dp as DP
 from . import engine as E
 from .config import cfg_get
 from .data import BatchLoader, ImageFolderDataset
@@ -71,6 +72,24 @@ class FlatAdam:
         if sd.get("param_groups"):
             g = sd["param_groups"][0]
             self.lr, self.betas, self.eps = g["lr"], tuple(g["betas"]), g["eps"]
+
+
+class _Segments:
+    """A recorded step: the library's launch recordings (`_lib.Recording`) and, under DP, the
+    exchange's host actions between them, re-issued in order."""
+
+    def __init__(self, segs):
+        self.segs = [x for x in segs if callable(x) or len(x) > 0]
+
+    def replay(self):
+        for x in self.segs:
+            if hasattr(x, "replay"):
+                x.replay()
+            else:
+                x()
+
+    def __len__(self):
+        return sum(len(x) for x in self.segs if hasattr(x, "replay"))
 
 
 class ProgressiveGAN:
@@ -309,20 +328,28 @@ class ProgressiveGAN:
     graph_replays = 0
 
     def _graph_key(self, eng, B):
-        """The key of a replayable step, or None when this step must run eagerly: one
-        process, the HIP op set (device-side step counters), no trace hook, packed weights,
-        no deferred generator update."""
-        if not ((self.use_graph or self.use_replay) and self._exchange is None and
+        """The key of a replayable step, or None when this step must run eagerly: the HIP op
+        set (device-side step counters), no trace hook, packed weights.  The hipGraph form:
+        one process, no deferred generator update.  The C++ replay also under DP: the
+        exchange's collectives and waits are host actions recorded between launch segments
+        (dp.GradExchange._act), and a deferred generator update is the exchange's own state."""
+        dp = self._exchange is not None
+        if not ((self.use_graph or self.use_replay) and
                 self.device.type == "cuda" and self.hyper.gp_mode == "r1" and
                 hasattr(eng.ops, "randn_dev") and hasattr(eng.ops, "adam_dev") and
-                eng.trace is None and eng.grad_ready is None and not E.FORCE_SERIAL and
-                eng._pending_G is None and all(eng._packed.values())):
+                eng.trace is None and not E.FORCE_SERIAL and all(eng._packed.values())):
+            return None
+        if dp:
+            if not self.use_replay or eng.grad_ready != self._exchange.ready or \
+                    not (eng._pending_G is None or isinstance(eng._pending_G, DP.Handle)):
+                return None
+        elif eng.grad_ready is not None or eng._pending_G is not None:
             return None
         h = self.hyper
         return ("replay" if self.use_replay else "graph",
                 id(eng), id(self.fpG), id(self.fpD), B, float(self.G.alpha), float(self.D.alpha),
                 h.lr_G, h.lr_D, h.beta1, h.beta2, h.eps, h.W_adv, h.slope_cfg, h.gp_mode, h.W_gp,
-                h.W_drift)
+                h.W_drift, id(self._exchange), isinstance(eng._pending_G, DP.Handle))
 
     def _step_body(self, eng, real, B):
         """The work of one step after the batch is resident: latents, then the engine step."""
@@ -348,11 +375,18 @@ class ProgressiveGAN:
     def _replay(self, eng, key, img_real, B):
         """Run the step from the captured graph (capturing it on the second step with the
         same key); returns the engine's outputs or None to run eagerly."""
-        gs = self.__dict__.setdefault("_gstate", {})
-        if gs.get("key") != key:
-            gs.clear()
-            gs["key"] = key          # first step with this key: eager (warms every lazy buffer)
+        # one state per key (a DP run alternates two: with and without a deferred generator
+        # update, e.g. around flush()); the first step of a key runs eagerly (warms every lazy
+        # buffer), the second records, later ones replay
+        states = self.__dict__.setdefault("_gstates", {})
+        gs = states.get(key)
+        if gs is None:
+            if len(states) >= 4:
+                states.clear()
+            states[key] = gs = {"key": key}
+            self._gstate = gs
             return None
+        self._gstate = gs
         # the graph's kernels read the device-side Adam step counts and RNG offset and advance
         # them, and a capture would record the host's re-sync of them (a fill) into the graph:
         # capture or replay only while the host's counts are the ones the device holds.  An
@@ -360,19 +394,33 @@ class ProgressiveGAN:
         # runs eagerly (which rewrites the device copies) and the next one captures again.
         if (any(fp._step_dev_host != fp.step for fp in (self.fpG, self.fpD)) or
                 getattr(self, "_rng_off_host", None) != self._rng_step * self._z.numel()):
-            gs.clear()
-            gs["key"] = key
+            states.clear()
+            states[key] = self._gstate = {"key": key}
             return None
         if key[0] == "replay":
             if "rec" not in gs:
                 # record the second step while it runs; the recording holds the buffer
-                # pointers of this batch, so later batches are copied into the same buffer
+                # pointers of this batch, so later batches are copied into the same buffer.
+                # Under DP the exchange's host actions split it into segments: C++ launch
+                # recordings and the Python collectives / waits between them.
                 gs["real"] = img_real if img_real is self.synthetic else img_real.clone()
+                segs = []
+
+                def hook(fn):
+                    segs.append(eng.ops.record_end())
+                    segs.append(fn)
+                    eng.ops.record_begin()
+
+                if self._exchange is not None:
+                    self._exchange.record_hook = hook
                 eng.ops.record_begin()
                 try:
                     gs["out"] = self._step_body(eng, gs["real"], B)
                 finally:
-                    gs["rec"] = eng.ops.record_end()
+                    segs.append(eng.ops.record_end())
+                    if self._exchange is not None:
+                        self._exchange.record_hook = None
+                    gs["rec"] = _Segments(segs)
                 return gs["out"]
             if img_real is not gs["real"]:
                 gs["real"].copy_(img_real)
@@ -426,6 +474,7 @@ class ProgressiveGAN:
         out = self._replay(eng, key, img_real, B) if key is not None else None
         if out is None:
             if key is None:        # an eager step may change what a captured graph assumed
+                self.__dict__.pop("_gstates", None)
                 self.__dict__.pop("_gstate", None)
             out = self._step_body(eng, img_real, B)
         img_real, _, img_fake = out

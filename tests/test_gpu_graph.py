@@ -128,3 +128,48 @@ def test_cpp_replay_matches_eager_bitwise(tmp_path, dtype):
     assert replayed == 3, replayed
     rec = rep._gstate.get("rec")
     assert rec is not None and len(rec) > 50, "recording holds the step's launches"
+
+
+@pytest.mark.parametrize("dtype", ["bf16"])
+def test_cpp_replay_under_dp_exchange_bitwise(tmp_path, dtype):
+    """The C++ replay with the DP exchange on (an RCCL group of one rank, the bench's
+    --dp-exchange): the exchange's collectives, seals and waits are host actions recorded
+    between the launch segments (dp.GradExchange._act), the G exchange deferred across the
+    step boundary (the second-backward reorder) -- against the same model stepped eagerly:
+    BITWISE equal after every step, with replays from the fourth step on."""
+    import torch.distributed as dist
+    from test_gpu_dp import _free_port
+    if not dist.is_initialized():
+        import os
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(_free_port())
+        dist.init_process_group("nccl", rank=0, world_size=1)
+        own = True
+    else:
+        own = False
+    try:
+        args = make_args(tmp_path, depths=list(TINY_DEPTHS), compute_dtype=dtype)
+        args.update({"dp_exchange_world1": True})
+        s = 3
+        eager, rep = build(args, False, s), build_replay(args, s)
+        for m in (eager, rep):
+            m.set_multi_GPU()
+            m.G.alpha = m.D.alpha = 0.5
+        replayed = 0
+        for step in range(8):
+            n0 = rep.graph_replays
+            eager.train_step()
+            rep.train_step()
+            replayed += rep.graph_replays - n0
+            if step == 7:
+                for m in (eager, rep):
+                    m.flush()
+            torch.cuda.synchronize()
+            a, b = state(eager), state(rep)
+            for k in a:
+                assert torch.equal(a[k], b[k]), (step, k, float((a[k].double() - b[k].double()).abs().max()))
+        assert replayed >= 4, replayed
+        assert rep._exchange.calls > 0
+    finally:
+        if own:
+            dist.destroy_process_group()
