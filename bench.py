@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--dp-exchange", action="store_true",
                    help="at one process: run the DP gradient exchange anyway (a one-rank RCCL "
                         "group), to measure the bookkeeping's cost against the plain step")
-    p.add_argument("--dp-bucket-mb", type=float, default=32.0,
+    p.add_argument("--dp-bucket-mb", type=float, default=64.0,
                    help="DP all-reduce bucket size (config dp_bucket_mb)")
     return p.parse_args()
 
@@ -383,6 +383,7 @@ def main():
     torch.cuda.synchronize()
     replays0 = model.graph_replays
     t0 = time.perf_counter()
+    hostlog = [] if os.environ.get("PG_BENCH_HOSTLOG") else None
     for i in range(args.steps):
         # per-launch HIP events on the conv kernels during the last timed step only: each
         # event pair costs ~7 us of GPU time, so instrumenting every step would cost ~10 %
@@ -391,7 +392,11 @@ def main():
         if timer and i == args.steps - 1:
             timer.on = True
             model.use_graph = model.use_replay = False
+        if hostlog is not None:
+            hostlog.append(time.perf_counter())
         step()
+    if hostlog is not None:   # when each step's host work started (ms from the first)
+        log("host step starts (ms): " + " ".join(f"{1e3 * (t - hostlog[0]):.2f}" for t in hostlog))
     model.flush()        # the last step's (deferred) generator update is part of the step
     torch.cuda.synchronize()
     if world > 1:

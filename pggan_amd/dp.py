@@ -89,9 +89,6 @@ class GradExchange:
         self.record_hook = None
         self.calls = 0          # collectives launched, and the host seconds spent in them
         self.host_s = 0.0
-        # set by the engine around ready(): called once before ready() launches a collective
-        # (the side stream's wait for the main stream, needed only then)
-        self.before_launch = None
 
     def bind(self, net, fp):
         """fp: the net's engine.FlatParams (live parameters first)."""
@@ -166,8 +163,6 @@ class GradExchange:
             st["pend"].append((lo, hi))
             st["pend_elems"] += hi - lo
         if st["pend_elems"] * 4 >= self.bucket_bytes:
-            if self.before_launch is not None:
-                self.before_launch()
             self._launch_merged(net, st["pend"])
             st["pend"], st["pend_elems"] = [], 0
 

@@ -921,34 +921,14 @@ class StepEngine:
         if self.side is None:
             self.grad_ready(net, names)
             return
-        # the gradients come from both streams: the side stream waits for the main one and
-        # the callback runs on it, so a collective it starts sees both without stalling the
-        # main stream's next convs.  A callback owner with a `before_launch` slot (dp.py's
-        # GradExchange) gets that wait as a hook it runs only when it launches a collective:
-        # most layers only add to a bucket, and each main-stream event record costs the main
-        # stream's next kernel ~6.5 us.
-        main = torch.cuda.current_stream()
-        owner = getattr(self.grad_ready, "__self__", None)
-        if owner is None or not hasattr(owner, "before_launch"):
-            self._side_wait_main()
-            with torch.cuda.stream(self.side):
-                self.grad_ready(net, names)
-            return
-
-        def sync():
-            ev = self._event(False)
-            if ev is None:
-                self.side.wait_stream(main)
-            else:
-                ev.record(main)
-                ev.wait(self.side)
-
-        owner.before_launch = sync
-        try:
-            with torch.cuda.stream(self.side):
-                self.grad_ready(net, names)
-        finally:
-            owner.before_launch = None
+        # every parameter gradient is written on the side stream (_side_call / _wgrad: the
+        # conv, linear, to/fromRGB weight and bias gradients; the zero fill before the step is
+        # ordered ahead of them by the side stream's wait for the main one at each launch), so
+        # the callback runs on the side stream and a collective it starts sees the finished
+        # gradients in stream order -- no main-stream event record (each costs the main
+        # stream's next kernel ~6.5 us; round 4 recorded one per bucket launch)
+        with torch.cuda.stream(self.side):
+            self.grad_ready(net, names)
 
     def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False,
                    gimg_overwrite=False, norms=None):

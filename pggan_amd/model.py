@@ -158,10 +158,11 @@ class ProgressiveGAN:
             from .dp import GradExchange
             rd = torch.bfloat16 if cfg_get(self.args, "dp_reduce_dtype", "f32") == "bf16" \
                 else torch.float32
-            # bucket size: config dp_bucket_mb (32 MiB).  Each collective costs ~50-100 us of
-            # host time (torch + RCCL enqueue); 4 MiB buckets made the host enqueue the step's
-            # bound (bench.py --dp-exchange)
-            mb = float(cfg_get(self.args, "dp_bucket_mb", 32))
+            # bucket size: config dp_bucket_mb (64 MiB).  Each collective costs ~50-100 us of
+            # host time (torch + RCCL enqueue) and ~0.15 % of the step at one rank (32 -> 64 MiB:
+            # 10 -> 5 collectives per step, -3.2 -> -2.5 %, profiles/r5_dp_ab.txt); the tail the
+            # last backward leaves for finish() is the last 512-channel layers either way
+            mb = float(cfg_get(self.args, "dp_bucket_mb", 64))
             self._exchange = GradExchange(self.world, bucket_bytes=int(mb * (1 << 20)),
                                           reduce_dtype=rd)
 

@@ -5,7 +5,7 @@
 #            replay with the collectives recorded between launch segments
 #   dpx_sync --dp-exchange, the G exchange waited for before the next step (no B2 reorder)
 #   dpx_eager --dp-exchange enqueued from Python every step
-#   dpx_b1g  --dp-exchange with 1 GiB buckets: one collective per net, at its end
+#   dpx_b64  --dp-exchange with 64 MiB buckets
 # 10 timed steps after 3 warm-up, ROUNDS rounds.  Log: gpurun_out/dp_ab.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -24,6 +24,5 @@ for i in $(seq "$rounds"); do
   ARGS="" run plain GPU_MAX_HW_QUEUES=4
   ARGS="--dp-exchange" run dpx GPU_MAX_HW_QUEUES=16
   ARGS="--dp-exchange" run dpx_sync GPU_MAX_HW_QUEUES=16 PG_ENGINE=overlap_g_exchange=0
-  ARGS="--dp-exchange --dp-bucket-mb 1024" run dpx_b1g GPU_MAX_HW_QUEUES=16
-  ARGS="--dp-exchange --dp-bucket-mb 1024" run dpx_b1g_sync GPU_MAX_HW_QUEUES=16 PG_ENGINE=overlap_g_exchange=0
+  ARGS="--dp-exchange --dp-bucket-mb 64" run dpx_b64 GPU_MAX_HW_QUEUES=16
 done
