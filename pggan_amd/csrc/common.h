@@ -153,9 +153,13 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // Instead every workgroup stores its totals into the caller's scratch (pg_scratch_bytes, one per
 // stream, zero-filled once) and the last workgroup to arrive sums them in workgroup order with a
 // fixed split over its threads: the result depends only on the launch geometry.
-// Hand-off (MI355X guide, in-launch split-K recipe): plain partial stores -> vmcnt(0) -> barrier
-// -> one lane's agent-scope release -> vmcnt(0) -> relaxed agent ticket; the drawer of the last
-// ticket acquires (agent) before reading the partials, and returns the ticket to 0.
+// Hand-off (MI355X guide, Guideline 16 R1): the partials are stored write-through (sc1, relaxed
+// agent-scope atomic stores) -> every wave's vmcnt(0) -> barrier -> one lane's relaxed agent
+// ticket; the drawer of the last ticket acquires (agent) and reads the partials with sc1 loads,
+// then returns the ticket to 0.  No release fence: an agent-scope release writes back the
+// whole XCD L2's dirty lines (buffer_wbl2), once per workgroup -- with the main stream's convs
+// writing beside these side-stream kernels that cost the 1x1 RGB weight gradient 84-175 us
+// per launch (kernel trace, profiles/r5_v2_*).
 constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
 __host__ __device__ constexpr size_t pg_scratch_floats() {
   return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
@@ -177,13 +181,12 @@ __device__ __forceinline__ void det_commit(const float* tot, int NA, float* scra
   const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
   float* part = pg_scratch_partials(scratch);
-  for (int q = tid; q < NA; q += nt) part[(size_t)bid * NA + q] = tot[q];
+  for (int q = tid; q < NA; q += nt)
+    __hip_atomic_store(part + (size_t)bid * NA + q, tot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ unsigned det_last;
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     det_last = (t == nb - 1) ? 1u : 0u;
   }
@@ -207,11 +210,13 @@ __device__ __forceinline__ void det_commit(const float* tot, int NA, float* scra
     for (; b + 8 <= b1; b += 8) {   // 8 loads in flight, summed in workgroup order
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(b + u) * NA + q];
+      for (int u = 0; u < 8; ++u)
+        v[u] = __hip_atomic_load(part + (size_t)(b + u) * NA + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
     }
-    for (; b < b1; ++b) s += part[(size_t)b * NA + q];
+    for (; b < b1; ++b)
+      s += __hip_atomic_load(part + (size_t)b * NA + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tmp[it] = s;
   }
   __syncthreads();
@@ -235,13 +240,11 @@ __device__ __forceinline__ void det_commit_seg(float v, int nseg, float* scratch
   const unsigned bid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   unsigned* ticket = reinterpret_cast<unsigned*>(scratch);
   float* part = pg_scratch_partials(scratch);
-  if (tid == 0) part[bid] = v;
+  if (tid == 0) __hip_atomic_store(part + bid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ unsigned det_last;
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     det_last = (t == nb - 1) ? 1u : 0u;
   }
@@ -260,17 +263,17 @@ __device__ __forceinline__ void det_commit_seg(float v, int nseg, float* scratch
   for (int it = tid; it < nseg * G; it += nt) {
     const int q = it % nseg, g = it / nseg;
     const unsigned j0 = g * per, j1 = j0 + per < seg ? j0 + per : seg;
-    const float* p = part + (size_t)q * seg;
+    float* p = part + (size_t)q * seg;
     float s = 0.f;
     unsigned j = j0;
     for (; j + 8 <= j1; j += 8) {
       float w[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) w[u] = p[j + u];
+      for (int u = 0; u < 8; ++u) w[u] = __hip_atomic_load(p + j + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += w[u];
     }
-    for (; j < j1; ++j) s += p[j];
+    for (; j < j1; ++j) s += __hip_atomic_load(p + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tmp[it] = s;
   }
   __syncthreads();
