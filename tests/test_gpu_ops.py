@@ -442,6 +442,10 @@ WIDE_CASES = [
     (4, 256, 64, 128, ("mask",)),
     (2, 512, 32, 64, ("bias", "lrelu", "pool")),
     (2, 512, 32, 64, ()),
+    # tile 15 (64 -> 32, CK = 64, persistent, compile-time flags): the G conv a at 512^2
+    (2, 512, 64, 32, ("ups", "bias", "lrelu", "pixnorm")),
+    # the 32^2 wide convs of the merged passes (B = 8) on the 16-row tile
+    (8, 32, 512, 512, ("bias", "lrelu")),
 ]
 
 
