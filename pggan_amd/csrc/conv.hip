@@ -1178,7 +1178,16 @@ __global__ __launch_bounds__(64 * G) void wgrad_slab_reduce(const float* ws, siz
   float s = 0.f;
   if (i < slab) {
     int k = s0;
-    for (; k + 4 <= s1; k += 4) {   // 4 loads in flight per round, summed in slab order
+    // 16 loads in flight per round, summed in slab order (the narrow layers' 512-1024 splits
+    // over 16 waves per block: 4 loads per round left a 16-round latency chain, ~18 us)
+    for (; k + 16 <= s1; k += 16) {
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = ws[(size_t)(k + u) * slab + i];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += t[u];
+    }
+    for (; k + 4 <= s1; k += 4) {
       float t[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) t[u] = ws[(size_t)(k + u) * slab + i];
