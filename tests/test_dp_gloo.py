@@ -130,3 +130,54 @@ def test_dp_overlap_is_bitwise_identical(tmp_path):
             assert np.array_equal(out[False][i][k], out[True][i][k]), (i, k)
             # bucketing changes which elements travel together, not the fp32 sums
             assert np.array_equal(out[False][i][k], out["bucketed"][i][k]), (i, k)
+
+
+def _replay_worker(rank, world, port, out_dir):
+    """GradExchange's host actions recorded during one exchange (the record_hook the C++ replay
+    uses) and re-run against new gradients give the eager exchange's result: the same buckets,
+    seal and wait, in order."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pggan_amd import engine as E
+    from pggan_amd.dp import GradExchange
+    shapes = E.d_param_shapes(TINY_DEPTHS, S)
+    fp = E.FlatParams(shapes, E.dead_params("D", S), "cpu",
+                      {k: torch.from_numpy(v) for k, v in make_params(shapes, seed=503).items()})
+    names = [n for n in fp.spans if n not in fp.dead]
+    ex = GradExchange(world, bucket_bytes=4 << 10)
+    ex.bind("D", fp)
+
+    def exchange(g):
+        fp.grad.copy_(g)
+        for n in reversed(names):     # backward order, a layer's weight and bias per call
+            ex.ready("D", [n])
+        h = ex.finish("D")
+        h.wait()
+        return fp.grad.clone()
+
+    gen = torch.Generator().manual_seed(rank)
+    g1, g2 = (torch.randn(fp.grad.shape, generator=gen) for _ in range(2))
+    acts = []
+    ex.record_hook = acts.append
+    r1 = exchange(g1)
+    ex.record_hook = None
+    fp.grad.copy_(g2)                 # replay the recorded actions on the next gradient
+    for fn in acts:
+        fn()
+    r2 = fp.grad.clone()
+    ref2 = exchange(g2)               # the same exchange run eagerly
+    torch.save(dict(r1=r1, r2=r2, ref2=ref2, n=len(acts)), os.path.join(out_dir, f"rep{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_recorded_exchange_actions_replay(tmp_path):
+    world = 2
+    mp.spawn(_replay_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [torch.load(tmp_path / f"rep{r}.pt", weights_only=True) for r in range(world)]
+    assert outs[0]["n"] >= 3, "buckets + seal + wait recorded"
+    for o in outs:
+        assert torch.equal(o["r2"], o["ref2"])
+        assert not torch.equal(o["r1"], o["r2"])
+    assert torch.equal(outs[0]["r2"], outs[1]["r2"])   # the mean over ranks on both
