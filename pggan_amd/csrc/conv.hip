@@ -1294,10 +1294,11 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // wave of workgroups; the HBM-bound narrow ones use ~4 per CU
   // (tools/wg_target_sweep.sh: 512 for the narrow tiles, 80.9 -> 59.2 us at 512^2 32->32,
   // 86 -> 79 at 1024^2 16->16, 108 -> 99 at 1024^2 16->32: half the slab traffic)
-#ifndef PG_AB_WG_WIDE_TARGET
-#define PG_AB_WG_WIDE_TARGET 256
-#endif
-  int target = pl.MO >= 4 ? PG_AB_WG_WIDE_TARGET : 512;
+  // wide: 192 rather than one workgroup per CU (256): the weight gradients run on the side
+  // stream beside the input-gradient chain, and leaving a quarter of the CUs to the main
+  // stream's launches measured +0.2-0.6 % per step in 5 of 5 interleaved rounds (128: -2.6 %;
+  // profiles/r5_dp_ab.txt section 9)
+  int target = pl.MO >= 4 ? 192 : 512;
   // the LDS-DMA narrow tiles (tools/wg_target_dma.sh): (2,2) at 512^2 in one round of
   // workgroups (8 waves at 164 VGPRs: one workgroup per CU), 51.0 -> 48.8 us at 32->32;
   // (1,1) at 1024^2 with ~4 per CU, 74.3 -> 62.7 us at 16->16
