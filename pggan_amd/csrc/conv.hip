@@ -1298,7 +1298,7 @@ WgbPlan wgrad_bf16_plan(const pg_conv_desc* d) {
   // stream beside the input-gradient chain, and leaving a quarter of the CUs to the main
   // stream's launches measured +0.2-0.6 % per step in 5 of 5 interleaved rounds (128: -2.6 %;
   // profiles/r5_dp_ab.txt section 9)
-  int target = pl.MO >= 4 ? 192 : 512;
+  int target = pl.MO >= 4 ? 192 : 512;   // narrow: 384 measured slower (r5_dp_ab.txt section 10)
   // the LDS-DMA narrow tiles (tools/wg_target_dma.sh): (2,2) at 512^2 in one round of
   // workgroups (8 waves at 164 VGPRs: one workgroup per CU), 51.0 -> 48.8 us at 32->32;
   // (1,1) at 1024^2 with ~4 per CU, 74.3 -> 62.7 us at 16->16
