@@ -160,6 +160,13 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // whole XCD L2's dirty lines (buffer_wbl2), once per workgroup -- with the main stream's convs
 // writing beside these side-stream kernels that cost the 1x1 RGB weight gradient 84-175 us
 // per launch (kernel trace, profiles/r5_v2_*).
+// The write-through hand-off is validated on gfx950 (and holds on gfx942, same cache
+// protocol); any other target gets the agent-scope release fence the memory model asks for.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#define PG_DET_RELEASE() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")
+#else
+#define PG_DET_RELEASE() ((void)0)
+#endif
 constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
 __host__ __device__ constexpr size_t pg_scratch_floats() {
   return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
@@ -184,6 +191,7 @@ __device__ __forceinline__ void det_commit(const float* tot, int NA, float* scra
   for (int q = tid; q < NA; q += nt)
     __hip_atomic_store(part + (size_t)bid * NA + q, tot[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PG_DET_RELEASE();
   __syncthreads();
   __shared__ unsigned det_last;
   if (tid == 0) {
@@ -242,6 +250,7 @@ __device__ __forceinline__ void det_commit_seg(float v, int nseg, float* scratch
   float* part = pg_scratch_partials(scratch);
   if (tid == 0) __hip_atomic_store(part + bid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PG_DET_RELEASE();
   __syncthreads();
   __shared__ unsigned det_last;
   if (tid == 0) {

@@ -147,11 +147,21 @@ class BatchLoader:
         self.gen = gen if gen is not None else torch.Generator().manual_seed(seed)
         self._pending = {}       # dataset index -> future of its decoded image
         self._ws = None
-        if cache_bytes is None:
-            cache_bytes = default_cache_bytes(self.dev)
-        self.cache = (HbmImageCache(len(dataset), dataset.size, self.dev, cache_bytes)
-                      if cache_bytes > 0 else None)
+        # the cache is allocated at the SECOND batch: the first one is drawn before the stage's
+        # training step has allocated its buffers (ProgressiveGAN.train_step builds the engine
+        # after load_next_batch), so a default budget sized from free memory then would take
+        # memory the step needs.  cache_bytes=0 turns it off (opt-out).
+        self._cache_bytes = cache_bytes
+        self._calls = 0
+        self.cache = None
         self.decoded = 0         # images decoded on the host so far
+
+    def _make_cache(self):
+        b = self._cache_bytes
+        if b is None:
+            b = default_cache_bytes(self.dev)
+        if b > 0:
+            self.cache = HbmImageCache(len(self.ds), self.ds.size, self.dev, b)
 
     def _cached(self, i):
         return self.cache is not None and self.cache.slot[i] >= 0
@@ -163,6 +173,9 @@ class BatchLoader:
                 self._pending[i] = self.pool.submit(self.ds.load, i)
 
     def next(self, idx, prefetch=None):
+        if self._calls == 1:
+            self._make_cache()
+        self._calls += 1
         idx = [int(i) for i in idx]
         self._submit(idx)
         B, S = len(idx), self.ds.size

@@ -1497,6 +1497,15 @@ class StepEngine:
         """Complete a deferred G update (overlapped DP mode); no-op otherwise."""
         self._finish_G()
 
+    def host_state(self):
+        """The Python-side schedule state a step leaves behind (ProgressiveGAN's C++ replay
+        runs no Python, so it restores this after re-issuing a recorded step)."""
+        return (self._pending_G, self._g_done, self._z_g, dict(self._packed))
+
+    def set_host_state(self, st):
+        self._pending_G, self._g_done, self._z_g, packed = st
+        self._packed = dict(packed)
+
     def params_changed(self):
         """Parameters were modified outside the engine (checkpoint load, broadcast):
         repack both nets at the next step."""

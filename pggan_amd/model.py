@@ -415,22 +415,37 @@ class ProgressiveGAN:
                 if self._exchange is not None:
                     self._exchange.record_hook = hook
                 eng.ops.record_begin()
+                steps0 = (self.fpG.step, self.fpD.step)
+                ok = False
                 try:
                     gs["out"] = self._step_body(eng, gs["real"], B)
+                    ok = True
                 finally:
                     segs.append(eng.ops.record_end())
                     if self._exchange is not None:
                         self._exchange.record_hook = None
-                    gs["rec"] = _Segments(segs)
+                    if ok:
+                        gs["rec"] = _Segments(segs)
+                        # the engine's host state after the step (a deferred generator update
+                        # under DP, the merged-forward flags): a replay runs no Python, so it
+                        # restores what the recorded step left behind.  The Adam steps the
+                        # recording runs: one per net, except under DP where a step that starts
+                        # with no deferred G update (after a flush) runs no Adam_G
+                        gs["post"] = eng.host_state()
+                        gs["adam"] = (self.fpG.step - steps0[0], self.fpD.step - steps0[1])
+                    else:       # a truncated recording is never replayed: the key starts over
+                        states.pop(key, None)
+                        self.__dict__.pop("_gstate", None)
                 return gs["out"]
             if img_real is not gs["real"]:
                 gs["real"].copy_(img_real)
             self._rng_step += 1
             self._rng_off_host = self._rng_step * self._z.numel()
-            for fp in (self.fpG, self.fpD):
-                fp.step += 1
+            for fp, n in zip((self.fpG, self.fpD), gs["adam"]):
+                fp.step += n
                 fp._step_dev_host = fp.step
             gs["rec"].replay()
+            eng.set_host_state(gs["post"])
             self.graph_replays += 1
             return gs["out"]
         if "graph" not in gs:

@@ -168,8 +168,10 @@ def test_batch_loader_end_to_end(tmp_path):
     ds = PD.ImageFolderDataset([str(tmp_path)], scale_index=3)      # 32 x 32
     assert len(ds) == 6
     batches = [[0, 1, 2, 3], [4, 5, 0, 1], [2, 3, 4, 5], [0, 1, 2, 3]]
-    # cache_bytes: room for 5 of the 6 images (index 5 is decoded every time it comes up),
-    # then no cache; 0: no cache.  Every batch is byte-exact either way.
+    # cache_bytes: room for 5 of the 6 images, then no cache; 0: no cache.  Every batch is
+    # byte-exact either way.  The cache is allocated at the second batch (after the stage's
+    # step has its buffers): batch 0 decodes 4, batch 1 decodes and caches 4, 5, 0, 1,
+    # batch 2 decodes 2 (cached, the fifth row) and 3 (no room), batch 3 decodes 3 again.
     for cache in (5 * 32 * 32 * 3, 0):
         ld = PD.BatchLoader(ds, "cuda", _lib.HipOps(torch.bfloat16), seed=4, workers=3,
                             cache_bytes=cache)
@@ -177,8 +179,7 @@ def test_batch_loader_end_to_end(tmp_path):
                 for k, b in enumerate(batches)]
         decoded = ld.decoded
         ld.close()
-        # with the cache only the first sight of each image and the uncached index 5 decode
-        assert decoded == (6 + 1 if cache else 16), decoded
+        assert decoded == (4 + 4 + 2 + 1 if cache else 16), decoded
         g = torch.Generator().manual_seed(4)
         for idx, out in zip(batches, outs):
             u8 = np.stack([ds.load(i) for i in idx])

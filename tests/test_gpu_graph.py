@@ -136,7 +136,11 @@ def test_cpp_replay_under_dp_exchange_bitwise(tmp_path, dtype):
     --dp-exchange): the exchange's collectives, seals and waits are host actions recorded
     between the launch segments (dp.GradExchange._act), the G exchange deferred across the
     step boundary (the second-backward reorder) -- against the same model stepped eagerly:
-    BITWISE equal after every step, with replays from the fourth step on."""
+    BITWISE equal after every step, with replays from the fourth step on.  flush() (what
+    save_checkpoint does, on rank 0 only in train.py) runs between steps four times at the same
+    key: the steps after a flush start with no deferred G update (the other recording), and a
+    replay must leave the engine's deferred-update state where the recorded step left it, or
+    the next step re-replays the no-pending recording and Adam_G never runs again."""
     import torch.distributed as dist
     from test_gpu_dp import _free_port
     if not dist.is_initialized():
@@ -156,19 +160,23 @@ def test_cpp_replay_under_dp_exchange_bitwise(tmp_path, dtype):
             m.set_multi_GPU()
             m.G.alpha = m.D.alpha = 0.5
         replayed = 0
-        for step in range(8):
+        for step in range(16):
             n0 = rep.graph_replays
             eager.train_step()
             rep.train_step()
             replayed += rep.graph_replays - n0
-            if step == 7:
+            if step in (6, 8, 10, 12, 15):
                 for m in (eager, rep):
                     m.flush()
             torch.cuda.synchronize()
             a, b = state(eager), state(rep)
             for k in a:
                 assert torch.equal(a[k], b[k]), (step, k, float((a[k].double() - b[k].double()).abs().max()))
-        assert replayed >= 4, replayed
+            ee, er = (next(iter(m._engines.values())) for m in (eager, rep))
+            assert (ee._pending_G is None) == (er._pending_G is None), step
+            assert eager.fpG.step == rep.fpG.step, step
+        assert int(rep.fpG.step_dev.item()) == rep.fpG.step
+        assert replayed >= 8, replayed
         assert rep._exchange.calls > 0
     finally:
         if own:
