@@ -189,6 +189,8 @@ ENGINE_DEFAULTS = dict(
     fuse_ubits=True,
     fuse_rgbbits=True,     # the top fromRGB output's sign bits (see _rgbbits)
     overlap_g_exchange=True,  # DP: the G all-reduce behind the next step's real-image part
+    tail_main=True,        # the last weight gradients of a final pass on the main stream
+    sep_b2=True,           # the merged second backward writes its own gradient buffers
 )
 
 
@@ -366,7 +368,7 @@ class StepEngine:
         # batch), self.dd holds first-half views (every batch-B pass: B1, the tangent, the G
         # half) and the generator's image is the second half of the merged input.  Needs
         # B % 4 == 0 so the minibatch-stddev groups (4 contiguous samples) stay within a half.
-        self.dd2 = None
+        self.dd2 = self.dd2b = None
         self._Bs = (B,)
         if merge_d:
             self._Bs = (B, 2 * B)
@@ -377,6 +379,13 @@ class StepEngine:
             self.dd2["xin"] = x3[:2 * B]
             self.dd = {k: v[:B] for k, v in self.dd2.items()}
             self.dd_hi = {k: v[B:] for k, v in self.dd2.items()}
+            # the merged second backward's gradient buffers: its own set, not the first-half
+            # views B1 wrote, so it does not wait for the tangent pass's weight terms (side
+            # stream) that still read B1's gradients (d_backward(join=False))
+            self.dd2b = dict(self.dd2)
+            if train and self.sep_b2:
+                for k in self._dgrad_keys():
+                    self.dd2b[k] = torch.zeros_like(self.dd2[k])
             g["img"] = x3[B:2 * B]
             if self.g2 is not None:
                 self.g2["img"] = x3[B:]
@@ -385,6 +394,13 @@ class StepEngine:
             self.dd = self._alloc_D(need_D, train)
         # losses: 0 L_real, 1 L_fake, 2 reg (R1 or GP), 3 L_G, 4 drift (wgan-gp mode)
         self.loss = torch.zeros(8, dtype=torch.float32, device=self.dev)
+
+    def _dgrad_keys(self):
+        """The D buffers a backward pass writes (d_backward)."""
+        ks = ["gzl1", "gzc", "gm", "gh", "gzrgb"] + (["gzd"] if self.s >= 1 else [])
+        for i in range(self.s):
+            ks += [f"gzb{i}", f"gza{i}", f"ghin{i}"]
+        return ks
 
     def _alloc_D(self, need_D, train, B=None):
         B = self.B if B is None else B
@@ -547,12 +563,13 @@ class StepEngine:
         return need
 
     def _wgrad(self, net, key, x, gz, dW, H, cin, cout, ups=False, db=None, gzbits=None,
-               gscale=1.0):
+               gscale=1.0, main=False):
         """gzbits: gz is the pooled-resolution gradient g and the conv's output gradient is
-        gscale * up2(g) * lrelu'(gzbits) (never materialised)."""
+        gscale * up2(g) * lrelu'(gzbits) (never materialised).  main: on the current stream
+        even with a side stream (the end of a final pass, _tail_main_on)."""
         c = self.packs[(net, key)][3]
         kw = dict(gzbits=gzbits, slope=SLOPE) if gzbits is not None else {}
-        if self.side is None or FORCE_SERIAL:
+        if self.side is None or FORCE_SERIAL or main:
             need = self._ws_need("w", H, cin, cout, ups)
             self.ops.conv_wgrad(x, gz, dW, B=self.B, H=H, W=H, cin=cin, cout=cout, ups=ups,
                                 scale=c * gscale, db=db, ws=self.ws if need else None, **kw)
@@ -606,6 +623,30 @@ class StepEngine:
                     cur.wait_event(ev)
                 else:
                     ev.wait(cur)
+
+    def _tail_main_on(self):
+        """Whether the final pass's last weight gradients run on the main stream."""
+        return self.side is not None and not FORCE_SERIAL and self.tail_main
+
+    def _tail_wait(self):
+        """Before a main-stream weight gradient of the final pass: the side-stream launches
+        issued before this pass (the tangent's weight terms it accumulates onto) are done."""
+        ev, self._tail_ev = getattr(self, "_tail_ev", None), None
+        if ev is not None:
+            cur = torch.cuda.current_stream()
+            if isinstance(ev, torch.cuda.Event):
+                cur.wait_event(ev)
+            else:
+                ev.wait(cur)
+
+    def _ready_main(self, net, *prefixes):
+        """grad_ready for gradients written on the main stream: the callbacks run on the
+        side stream (_ready), which first waits for the main one."""
+        if self.grad_ready is None:
+            return
+        if self.side is not None:
+            self._side_wait_main()
+        self._ready(net, *prefixes)
 
     def _conv_sup(self):
         """ops.conv_supported at every batch size the D passes run (B, and 2B when the D
@@ -856,21 +897,32 @@ class StepEngine:
         fb = "first_block.block.0.module."
         self._g_pn_bwd("first", g["u0"], g["y0"], g["r0"], g["gy0"], g["gz0"], 4, d[0], d[0],
                        L.CONV_LRELU)
-        self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
-                    db=GR[fb + "bias"])
-        self._ready("G", fb)
+        # the input-gradient chain ends at the latent: with tail_main the last two weight
+        # gradients run on the main stream after it while the side stream drains its queue
+        tail = self._tail_main_on()
+        if not tail:
+            self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
+                        db=GR[fb + "bias"])
+            self._ready("G", fb)
         self._conv("G", "first", g["gz0"], g["gh0"], 4, d[0], d[0], 0, dgrad=True)
         ops.pixnorm_lrelu_bwd(g["f"], g["gh0"], g["gzf"], d[0], self.hyper.slope_cfg)
-        self._side_call(("G",), ops.linear_wgrad,
-                        g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
-                        GR["latent_format_layer.module.bias"], B=B, flags=L.LIN_OUT_CHW,
-                        scale=he(self.latent))
-        self._ready("G", "latent_format_layer.module.")
+        lin = (g["zn"], g["gzf"], GR["latent_format_layer.module.weight"],
+               GR["latent_format_layer.module.bias"])
+        lkw = dict(B=B, flags=L.LIN_OUT_CHW, scale=he(self.latent))
+        if tail:
+            self._wgrad("G", "first", g["h0"], g["gz0"], GR[fb + "weight"], 4, d[0], d[0],
+                        db=GR[fb + "bias"], main=True)
+            ops.linear_wgrad(*lin, **lkw)
+            self._ready_main("G", fb, "latent_format_layer.module.")
+        else:
+            self._side_call(("G",), ops.linear_wgrad, *lin, **lkw)
+            self._ready("G", "latent_format_layer.module.")
 
     # ================================================================== D
-    def d_forward(self, P, img, alpha):
+    def d_forward(self, P, img, alpha, join=True):
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
-        self._side_join("D")
+        if join:
+            self._side_join("D")
         fr = "fromRGB_blocks.{}.fromRGB.module."
         ops.from_rgb(img, P[fr.format(s) + "weight"], P[fr.format(s) + "bias"], he(3), D["yrgb"],
                      B=B, R=R, C=d[s], down=False, slope=SLOPE,            # nets.py:255
@@ -931,15 +983,23 @@ class StepEngine:
             self.grad_ready(net, names)
 
     def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False,
-                   gimg_overwrite=False, norms=None):
+                   gimg_overwrite=False, norms=None, join=True):
         """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
         gimg: accumulate dL/dimg (zeroed by the caller unless gimg_overwrite: the first
         fromRGB input gradient then writes it); norms: += per-sample sum of dL/dimg^2, fused
         into the last pass writing gimg; keeps every gz.  img: the D input (a tensor or an
         _lib.ImgMix) for the fromRGB weight gradients.
-        final: the last pass writing D's gradients this half-step (grad_ready calls)."""
+        final: the last pass writing D's gradients this half-step (grad_ready calls); its top
+        level's conv-a and fromRGB weight gradients run on the main stream (_tail_main).
+        join=False: the pass writes buffers no pending side-stream launch reads (the merged
+        second backward's own set, dd2b)."""
         ops, D, d, s, B, R = self.ops, self.dd, self.depths, self.s, self.B, self.R
-        self._side_join("D")
+        if join:
+            self._side_join("D")
+        # the side-stream point after every weight term issued so far (the tangent's): a
+        # main-stream weight gradient accumulating onto one of them waits for it
+        self._tail_ev = self._side_ev.get("D")
+        tail = final and GR is not None and self._tail_main_on()
         ready = (lambda *p: self._ready("D", *p)) if final else (lambda *p: None)
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
@@ -1000,7 +1060,8 @@ class StepEngine:
                 self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
             hin = D["yrgb"] if i == s - 1 else (self._top_out(alpha) if i == s - 2 else D[f"p{i + 1}"])
-            if GR is not None:
+            top_tail = tail and i == s - 1
+            if GR is not None and not top_tail:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
                             d[i + 1],
                             db=GR[a + "bias"])
@@ -1015,12 +1076,24 @@ class StepEngine:
                 self._conv("D", f"a{i}", D[f"gza{i}"], D[f"ghin{i}"], Ri, d[i + 1], d[i + 1], 0,
                            dgrad=True)
                 g = D[f"ghin{i}"]
+            if top_tail:
+                # the input-gradient chain ends here: this weight gradient on the main stream
+                # (idle otherwise) while the side stream drains its queue
+                self._tail_wait()
+                self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
+                            d[i + 1], db=GR[a + "bias"], main=True)
+                self._ready_main("D", a)
         if s == 0:
             ops.unpool_mask(D["gh"], D["yrgb"], D["gzrgb"], B=B, H=4, W=4, C=d[0], scale=1.0,
                             slope=SLOPE, ups=False)
         fr = "fromRGB_blocks.{}.fromRGB.module."
         w = P[fr.format(s) + "weight"]
-        if GR is not None:
+        if GR is not None and tail and gimg is None:
+            self._tail_wait()
+            ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
+                             dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
+            self._ready_main("D", fr.format(s))
+        elif GR is not None:
             # img may be the generator's output buffer (fake pass): pending for both nets
             self._side_call(("D", "G"), ops.from_rgb_bwd,
                             D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
@@ -1198,10 +1271,11 @@ class StepEngine:
         return self.hyper.gp_mode == "r1" or not hasattr(self._pending_G, "wait")
 
     @contextlib.contextmanager
-    def _pair(self):
-        """Run the enclosed passes at batch 2B on the merged buffers."""
+    def _pair(self, b2=False):
+        """Run the enclosed passes at batch 2B on the merged buffers (b2: the second
+        backward's own gradient buffers)."""
         saved = (self.dd, self.B)
-        self.dd, self.B = self.dd2, 2 * saved[1]
+        self.dd, self.B = (self.dd2b if b2 else self.dd2), 2 * saved[1]
         try:
             yield
         finally:
@@ -1257,7 +1331,7 @@ class StepEngine:
             ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u"][B:], None)
             self.h_mb = h2
             try:
-                with self._pair():
+                with self._pair(b2=True):
                     self.d_backward(PD, GD, D2["u"], alpha_D, img=X)
             finally:
                 self.h_mb = h2[:B]
@@ -1271,9 +1345,10 @@ class StepEngine:
         ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
         self.h_mb = h2
         try:
-            with self._pair():
+            with self._pair(b2=True):
                 # D2["inj"]: the tangent wrote the real half; the fake half stays zero
-                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True)
+                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True,
+                                join=not self.sep_b2)
         finally:
             self.h_mb = h2[:B]
         self._side_join()
@@ -1336,15 +1411,18 @@ class StepEngine:
         img_fake = self._g_forward_d_half(PG, z, alpha_G)                       # :226-227
         self.dd = self.dd_hi
         try:
-            self.d_forward(PD, X[B:], alpha_D)                                   # :228
+            # writes second-half activations only: the tangent's weight terms still running
+            # on the side stream read first-half buffers, so no join
+            self.d_forward(PD, X[B:], alpha_D, join=not self.sep_b2)             # :228
         finally:
             self.dd = D1
         ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u2"][B:], None)
         self.h_mb = D2[self.h_mb_key]
         try:
-            with self._pair():
+            with self._pair(b2=True):
                 # D2["inj"]: the tangent wrote the real half; the fake half stays zero
-                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True)
+                self.d_backward(PD, GD, D2["u2"], alpha_D, img=X, inj_mbstd=D2["inj"], final=True,
+                                join=not self.sep_b2)
         finally:
             self.h_mb = D1[self.h_mb_key]
         self._side_join()

@@ -13,16 +13,18 @@ injected flips to rounding):
   C4 runs its per-GPU shard (B=8 at 512^2: the DP contract makes each rank's step the
   single-process step on its shard, tests/test_dp_gloo.py).
 * bf16 mode (the benchmarked path, C5 = the bench workload), the oracle fed our fake
-  images so each network sees identical inputs: images within 5% relative L2, losses
-  and R1 within 2% relative, every live gradient tensor at cosine >= 0.99 with the
+  images so each network sees identical inputs: images within 3% relative L2, losses
+  and R1 within 2e-3 relative, every live gradient tensor at cosine >= 0.999 with the
   oracle, injected flips on <= 1% of pre-activations and only at |x| <= 0.3 RMS (bf16
-  storage and weights round to 2^-9 and the error compounds over 18 layers; measured:
-  images 2%, losses <= 5e-4, worst cosine 0.99986, 0.15% flips, worst at 0.16 RMS).
+  storage and weights round to 2^-9 and the error compounds over 18 layers; measured in
+  round 2: images 2%, losses <= 5e-4, worst cosine 0.99986, 0.15% flips, worst at 0.16
+  RMS; the bars sit near what the kernels achieve so a regression shows, round-6 reports:
+  profiles/r6_parity_*.json).
 
 Inputs: numpy PCG64 seeds (tests/golden/gen_inputs.py): weights N(0,1) like the
 reference init (lib/layers.py:51-56), biases 0.1*N(0,1) so the bias*c path is live,
 reals U[-1,1), latents N(0,1).  If PG_PARITY_OUT names a directory, a JSON report per
-config is written there (profiles/r2_parity_*.json are copies).
+config is written there (profiles/r6_parity_*.json are copies).
 """
 import json
 import os
@@ -129,11 +131,11 @@ def test_bf16_bench_path_matches_oracle_at_c5():
     real, z1, z2 = (torch.from_numpy(st[k]) for k in ("real", "z1", "z2"))
     ours, ref, kinks = K.run_step(eng, fpG, fpD, real, z1, z2, alpha, threads=THREADS,
                                   feed_images=True)
-    rep = K.compare_bf16(ours, ref, fpG, fpD, kinks, loss_rtol=2e-2, min_cos=0.99,
-                         flip_bound=K.FLIP_BOUND[torch.bfloat16], img_rtol=5e-2,
+    rep = K.compare_bf16(ours, ref, fpG, fpD, kinks, loss_rtol=2e-3, min_cos=0.999,
+                         flip_bound=K.FLIP_BOUND[torch.bfloat16], img_rtol=3e-2,
                          what="C5 bf16: ")
     msg = K.summarize(rep)
     print(f"\nC5 bf16: {msg}", flush=True)
     _report("C5_bf16", rep, dict(config="C5", stage=s, batch=B, alpha=alpha, mode="bf16",
-                                 oracle="float64 + injected kinks", loss_rtol=2e-2,
-                                 min_cos=0.99, summary=msg))
+                                 oracle="float64 + injected kinks", loss_rtol=2e-3,
+                                 min_cos=0.999, img_rtol=3e-2, summary=msg))
