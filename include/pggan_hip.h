@@ -93,6 +93,13 @@ size_t pg_scratch_bytes(void);
  * gradient through an upsampling conv a, then the previous block's PixelNorm).  Not with
  * BIAS / MASK / ACCUM / PIXNORM / bit flags. */
 #define PG_CONV_PNBWD 2048
+/* fromRGB weight gradient in the epilogue of the input-gradient conv that produces the
+ * fromRGB output's gradient gz (the discriminator's top conv a, lib/blocks.py:153-170 with
+ * pggan/nets.py:255): the conv result gz is NOT stored; instead
+ *   dw[n*3 + i] += s * sum_pix gz[n] * img[i],  db[n] += s * sum_pix gz[n]
+ * (img fp32 NCHW [B][3][H][W], summed over workgroups in a fixed order through `scratch`).
+ * Only through pg_conv3x3_rgbw; query pg_conv3x3_supported. */
+#define PG_CONV_RGBW 4096
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -136,6 +143,14 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
 int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
                       const void* wpk, const float* bias, const void* aux, void* y, void* y2,
                       void* ws, size_t ws_bytes, void* stream);
+/* The input-gradient conv of PG_CONV_RGBW (d->flags includes it, y is not written): x, wpk,
+ * aux as pg_conv3x3_fwd; img the fromRGB layer's input image, s its He constant, dw [C*3] /
+ * db [C] the fromRGB weight / bias gradients (accumulated), scratch a PG_SCRATCH_BYTES
+ * reduction scratch of the stream.  Replaces pg_conv3x3_fwd + pg_from_rgb_bwd(dw, db) of the
+ * final backward pass (lib/model.py:95-97 through autograd in the reference). */
+int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const void* aux, const float* img, float s, float* dw, float* db,
+                    void* scratch, void* stream);
 /* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
  * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);

@@ -50,7 +50,23 @@ struct ConvParams {
   int xcd_remap;      // conv3x3_kernel: XCD-aware workgroup order
   int diag;           // conv_hr: timing diagnostics (PG_HR_DIAG), 0 in every real launch
   int tpw;            // conv_hr 8-wave LDS-DMA tile: tiles per workgroup (> 1: persistent form)
+  // PG_CONV_RGBW (conv_hr EF tiles): fromRGB weight gradient of the conv result
+  const float* rimg;  // fp32 NCHW [B][3][H][W]
+  float* rdw;         // [cout][3], accumulated
+  float* rdb;         // [cout], accumulated
+  float* scratch;     // det_commit scratch of the stream
+  float rscale;
 };
+
+// the RGBW operands of the next conv_hr launch on this host thread (pg_conv3x3_rgbw)
+struct RgbwArgs {
+  const float* img = nullptr;
+  float* dw = nullptr;
+  float* db = nullptr;
+  float* scratch = nullptr;
+  float s = 0.f;
+};
+static thread_local RgbwArgs g_rgbw;
 
 int cinp_of(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
 __device__ __forceinline__ int cinp_of_dev(int c) { return c <= 16 ? ((c + 7) & ~7) : ((c + 31) & ~31); }
@@ -1688,6 +1704,12 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
+  if (d->flags & PG_CONV_RGBW) {   // the EF tiles 0 / 5 (16 / 32 channels, H >= 512 here)
+    if constexpr (sizeof(T) != 2) return false;
+    if (d->flags != (PG_CONV_RGBW | PG_CONV_MASK | PG_CONV_AUX_BITS) || !conv_hr_ok(d)) return false;
+    const int t = conv_hr_tile(d);
+    return (t == 0 && d->cout == 16) || (t == 5 && d->cout == 32);
+  }
   if (d->flags & PG_CONV_PNBWD) {   // conv_hr epilogue, [cout][pixel] tiles of <= 32 channels
     if constexpr (sizeof(T) != 2) return false;
     if (d->flags & (BITS | PG_CONV_BIAS | PG_CONV_MASK | PG_CONV_ACCUM | PG_CONV_PIXNORM))
@@ -1845,6 +1867,23 @@ int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const voi
   PG_CHECK_ARG(x && wpk && y && d->cout % 4 == 0 && d->x_cs % 8 == 0 && d->y_cs >= d->cout,
                "conv3x3_fwd_ex: bad args");
   return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, (hipStream_t)stream, xbits);
+}
+
+int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const void* aux, const float* img, float s, float* dw, float* db,
+                    void* scratch, void* stream) {
+  PG_CHECK_ARG(d && x && wpk && aux && img && dw && scratch, "conv3x3_rgbw: null pointer");
+  PG_CHECK_ARG(dtype == PG_BF16 && (d->flags & PG_CONV_RGBW) && conv_supported<bf16_t>(d, 0),
+               "conv3x3_rgbw: flags 0x%x not supported for %d -> %d at %dx%d", d->flags, d->cin,
+               d->cout, d->H, d->W);
+  PG_CHECK_ARG(d->x_cs >= cinp_of(d->cin) && d->x_cs % 8 == 0 && d->aux_cs * 8 >= d->cout,
+               "conv3x3_rgbw: bad channel strides");
+  PG_CHECK_ARG(pg_det_fits((size_t)256 * 8, (size_t)d->cout * 4), "conv3x3_rgbw: scratch too small");
+  g_rgbw.img = img; g_rgbw.dw = dw; g_rgbw.db = db; g_rgbw.scratch = (float*)scratch; g_rgbw.s = s;
+  const int rc = conv_dispatch<bf16_t>(d, x, wpk, nullptr, aux, nullptr, nullptr, nullptr, 0,
+                                       (hipStream_t)stream);
+  g_rgbw = RgbwArgs{};
+  return rc;
 }
 
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes) {

@@ -191,6 +191,7 @@ ENGINE_DEFAULTS = dict(
     overlap_g_exchange=True,  # DP: the G all-reduce behind the next step's real-image part
     tail_main=True,        # the last weight gradients of a final pass on the main stream
     sep_b2=True,           # the merged second backward writes its own gradient buffers
+    fuse_rgbw=True,        # the final pass's fromRGB weight gradient in the top conv's epilogue
 )
 
 
@@ -717,6 +718,20 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
+    def _rgbw(self):
+        """Whether the final backward pass computes the top fromRGB weight / bias gradients in
+        the epilogue of the top conv a's input gradient (PG_CONV_RGBW: that gradient, which only
+        the fromRGB weight gradient reads in this pass, is never written)."""
+        key = ("rgbw", 0, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = self._conv_sup()
+            d, s, R, B = self.depths, self.s, self.R, self.B
+            ok = bool(self.fuse_rgbw and self._rgbbits() and hasattr(self.ops, "conv3x3_rgbw") and
+                      f(B=B, H=R, W=R, cin=d[s], cout=d[s],
+                        flags=L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_RGBW))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _pn_pool(self, i):
         """Whether level i's conv-a input gradient (pooled to level i-1) also applies level
         i-1's conv-b PixelNorm + LReLU backward (PG_CONV_POOL | PG_CONV_PNBWD): level i-1's
@@ -1000,6 +1015,9 @@ class StepEngine:
         # main-stream weight gradient accumulating onto one of them waits for it
         self._tail_ev = self._side_ev.get("D")
         tail = final and GR is not None and self._tail_main_on()
+        fr = "fromRGB_blocks.{}.fromRGB.module."
+        rgbw = (tail and gimg is None and s >= 1 and isinstance(img, torch.Tensor) and
+                self._rgbw())
         ready = (lambda *p: self._ready("D", *p)) if final else (lambda *p: None)
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
@@ -1066,7 +1084,15 @@ class StepEngine:
                             d[i + 1],
                             db=GR[a + "bias"])
                 ready(a)
-            if i == s - 1 and self._rgbbits():
+            if i == s - 1 and rgbw:
+                # the fromRGB weight gradient in this conv's epilogue: its result is not stored
+                self._tail_wait()   # after the tangent's fromRGB weight term (side stream)
+                fw = fr.format(s)
+                ops.conv3x3_rgbw(D[f"gza{i}"], self.packs[("D", f"a{i}")][1], B=B, H=Ri, W=Ri,
+                                 cin=d[i + 1], cout=d[i + 1], flags=L.CONV_MASK | L.CONV_AUX_BITS,
+                                 slope=SLOPE, aux=D["rgbb"], img=img, s=he(3),
+                                 dw=GR[fw + "weight"], db=GR[fw + "bias"])
+            elif i == s - 1 and self._rgbbits():
                 self._conv("D", f"a{i}", D[f"gza{i}"], D["gzrgb"], Ri, d[i + 1], d[i + 1],
                            L.CONV_MASK | L.CONV_AUX_BITS, aux=D["rgbb"], dgrad=True)
             elif i == s - 1:
@@ -1088,7 +1114,9 @@ class StepEngine:
                             slope=SLOPE, ups=False)
         fr = "fromRGB_blocks.{}.fromRGB.module."
         w = P[fr.format(s) + "weight"]
-        if GR is not None and tail and gimg is None:
+        if rgbw:
+            self._ready_main("D", fr.format(s))
+        elif GR is not None and tail and gimg is None:
             self._tail_wait()
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
                              dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])

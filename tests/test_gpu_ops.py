@@ -938,3 +938,45 @@ def test_pixnorm_bwd_fused_dgrad(B, H, C):
     torch.cuda.synchronize()
     cmp(out, ref, 1e-2, f"fused PNBWD H={H} C={C}")
     cmp(out, unf.float().cpu(), 2e-2, f"fused vs unfused H={H} C={C}")
+
+
+@pytest.mark.parametrize("B,H,C", [(2, 1024, 16), (2, 512, 32), (1, 512, 32)])
+def test_conv_rgbw_epilogue(B, H, C):
+    """PG_CONV_RGBW (bf16): the top conv a's input gradient with the fromRGB weight / bias
+    gradients in its epilogue (dw[n*3+i] += s sum gz[n] img[i], db[n] += s sum gz[n]; the
+    result gz is not stored) against the same conv on the CPU double (fp32 on the same bf16
+    operands and sign bits) followed by the float64 sums, accumulated onto existing values
+    (the tangent's term is already in the gradient); and bitwise reproducible."""
+    from cpu_ops import CONV_AUX_BITS, CONV_MASK
+    hip, cpu = ops_pair(torch.bfloat16)
+    fl = CONV_MASK | CONV_AUX_BITS
+    assert hip.conv_supported(B=B, H=H, W=H, cin=C, cout=C, flags=fl | _lib_flag("CONV_RGBW"))
+    dt = torch.bfloat16
+    x = q(rnd(B, H, H, C, seed=131), dt)
+    wd = q(rnd(r16(C) * 9 * cinp(C), seed=132, scale=0.05), dt)
+    bits = torch.randint(0, 256, (B, H, H, C // 8), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(133))
+    img = rnd(B, 3, H, H, seed=134)
+    dw0, db0 = rnd(C * 3, seed=135), rnd(C, seed=136)
+    s = 0.8165
+    gz = torch.zeros(B, H, H, C)
+    cpu.conv3x3(x.float(), wd.float(), gz, B=B, H=H, W=H, cin=C, cout=C, flags=fl, aux=bits)
+    g64, i64 = gz.double(), img.double()
+    dw_ref = dw0.double().view(C, 3) + s * torch.einsum("bhwn,bihw->ni", g64, i64)
+    db_ref = db0.double() + s * g64.sum(dim=(0, 1, 2))
+    outs = []
+    for _ in range(2):
+        dw, db = dw0.clone().cuda(), db0.clone().cuda()
+        hip.conv3x3_rgbw(x.to(dt).cuda(), wd.to(dt).cuda(), B=B, H=H, W=H, cin=C, cout=C, flags=fl,
+                         aux=bits.cuda(), img=img.cuda(), s=s, dw=dw, db=db)
+        outs.append((dw.cpu(), db.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), \
+        "RGBW sums not bitwise reproducible"
+    for got, ref, what in ((outs[0][0].view(C, 3), dw_ref, "dw"), (outs[0][1], db_ref, "db")):
+        err = float((got.double() - ref).norm() / ref.norm())
+        assert err <= 1e-4, (what, err)
+
+
+def _lib_flag(name):
+    from pggan_amd import _lib
+    return getattr(_lib, name)
