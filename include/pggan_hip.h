@@ -151,13 +151,6 @@ int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const voi
 int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                     const void* aux, const float* img, float s, float* dw, float* db,
                     void* scratch, void* stream);
-/* pg_conv3x3_fwd_ex with the stream's reduction scratch (PG_SCRATCH_BYTES): the bf16 4^2-16^2
- * convs (no PixelNorm / bit flags) split K over workgroups and combine the partial tiles in
- * the same launch, in a fixed order (deterministic), with per-tile tickets in the scratch;
- * ws must hold pg_conv3x3_workspace_size bytes.  scratch == NULL: pg_conv3x3_fwd_ex. */
-int pg_conv3x3_fwd2(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
-                    const void* wpk, const float* bias, const void* aux, void* y, void* y2,
-                    void* ws, size_t ws_bytes, void* scratch, void* stream);
 /* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
  * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);

@@ -97,8 +97,6 @@ _SIGS = {
     "pg_conv3x3_fwd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP],
                        _I),
     "pg_conv3x3_supported": ([_I, ctypes.POINTER(ConvDesc), _SZ], _I),
-    "pg_conv3x3_fwd2": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
-                         _SZ, _VP, _VP], _I),
     "pg_conv3x3_rgbw": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP],
                         _I),
     "pg_conv3x3_fwd_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
@@ -405,9 +403,9 @@ class HipOps:
                      y2.shape[-1] if y2 is not None else 0, flags, slope, out_scale,
                      xbits.shape[-1] if xbits is not None else 0)
         wsb = ws.numel() * ws.element_size() if ws is not None else 0
-        self._chk(self.lib.pg_conv3x3_fwd2(self._dt(y), ctypes.byref(d), _p(x), _p(xbits),
-                                           _p(wpk), _p(bias), _p(aux), _p(y), _p(y2), _p(ws),
-                                           wsb, self._scr(), self._s()),
+        self._chk(self.lib.pg_conv3x3_fwd_ex(self._dt(y), ctypes.byref(d), _p(x), _p(xbits),
+                                             _p(wpk), _p(bias), _p(aux), _p(y), _p(y2), _p(ws),
+                                             wsb, self._s()),
                   "conv3x3_fwd")
 
     def conv3x3_rgbw(self, x, wpk, *, B, H, W, cin, cout, flags, aux, img, s, dw, db,

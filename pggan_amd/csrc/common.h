@@ -168,10 +168,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 #define PG_DET_RELEASE() ((void)0)
 #endif
 constexpr int PG_SCRATCH_HDR_FLOATS = 16;   // ticket word + padding (64 B)
-// the last PG_SK_TICKETS words: per-tile tickets of the split-K convs (conv_sk.inc)
-constexpr int PG_SK_TICKETS = 4096;
 __host__ __device__ constexpr size_t pg_scratch_floats() {
-  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS - PG_SK_TICKETS;
+  return (PG_SCRATCH_BYTES / sizeof(float)) - PG_SCRATCH_HDR_FLOATS;
 }
 __host__ __device__ inline float* pg_scratch_partials(float* scratch) {
   return scratch + PG_SCRATCH_HDR_FLOATS;

@@ -1597,14 +1597,10 @@ int conv_splits(const pg_conv_desc* d) {
   return pg_cdiv(nch, cps);
 }
 
-size_t conv_sk_ws_bytes(const pg_conv_desc* d);
-
 size_t conv_ws_bytes(const pg_conv_desc* d) {
   const int sp = conv_splits(d);
-  const size_t sk = conv_sk_ws_bytes(d);
-  if (sp <= 1) return sk;
-  const size_t n = (size_t)sp * d->B * d->H * d->W * ((d->cout + 15) & ~15) * sizeof(float);
-  return n > sk ? n : sk;
+  if (sp <= 1) return 0;
+  return (size_t)sp * d->B * d->H * d->W * ((d->cout + 15) & ~15) * sizeof(float);
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR, int CKC = 0, int TWC = 0,
@@ -1701,7 +1697,6 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 
 #include "conv_hr.inc"
 #include "conv_lr.inc"
-#include "conv_sk.inc"
 #include "wgrad_dma.inc"
 
 
@@ -1749,14 +1744,10 @@ bool conv_supported(const pg_conv_desc* d, size_t wsb) {
 template <typename T>
 int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const float* bias,
                   const void* aux, void* y, void* y2, void* ws, size_t wsb, hipStream_t st,
-                  const void* xbits = nullptr, float* scratch = nullptr) {
+                  const void* xbits = nullptr) {
   PG_CHECK_ARG(conv_supported<T>(d, wsb), "conv3x3_fwd: flags 0x%x not supported for cout %d at %dx%d",
                d->flags, d->cout, d->H, d->W);
   if constexpr (sizeof(T) == 2) {
-    if (scratch && conv_sk_plan(d).ok) {   // 4^2-16^2: split K with the in-launch combine
-      const int rc = conv_sk_dispatch(d, x, wpk, bias, aux, y, y2, ws, wsb, scratch, st);
-      if (rc != PG_ERR_UNSUPPORTED) return rc;
-    }
     if (conv_lr_ok(d)) return conv_lr_dispatch(d, x, wpk, bias, aux, y, y2, st);
     if (conv_hr_ok(d)) return conv_hr_dispatch(d, x, wpk, bias, aux, y, y2, xbits, st);
   }
@@ -1865,21 +1856,6 @@ int pg_conv3x3_fwd(int dtype, const pg_conv_desc* d, const void* x, const void* 
   hipStream_t st = (hipStream_t)stream;
   if (dtype == PG_F32) return conv_dispatch<float>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
   return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, st);
-}
-
-int pg_conv3x3_fwd2(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
-                    const void* wpk, const float* bias, const void* aux, void* y, void* y2,
-                    void* ws, size_t ws_bytes, void* scratch, void* stream) {
-  if (!scratch || dtype != PG_BF16 || !d || !conv_sk_plan(d).ok)
-    return pg_conv3x3_fwd_ex(dtype, d, x, xbits, wpk, bias, aux, y, y2, ws, ws_bytes, stream);
-  PG_CHECK_ARG(x && wpk && y && d->cout % 4 == 0 && d->x_cs % 8 == 0 && d->y_cs >= d->cout,
-               "conv3x3_fwd2: bad args");
-  PG_CHECK_ARG(!(d->flags & PG_CONV_BIAS) || bias, "conv3x3_fwd2: BIAS flag without bias");
-  PG_CHECK_ARG(!(d->flags & PG_CONV_MASK) || (aux && d->aux_cs >= d->cout),
-               "conv3x3_fwd2: MASK flag without aux");
-  PG_CHECK_ARG(!y2 || (d->flags & PG_CONV_POOL), "conv3x3_fwd2: y2 only with POOL here");
-  return conv_dispatch<bf16_t>(d, x, wpk, bias, aux, y, y2, ws, ws_bytes, (hipStream_t)stream,
-                               nullptr, (float*)scratch);
 }
 
 int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const void* xbits,
@@ -2030,8 +2006,6 @@ void plan_conv(int dtype, pg_conv_desc* d, int* path, int* tile, size_t* ws) {
   *path = 0;
   *tile = -1;
   if (dtype == PG_BF16) {
-    const SkPlan sk = conv_sk_plan(d);
-    if (sk.ok && sk.S > 1) { *path = 3; *ws = conv_sk_ws_bytes(d); return; }
     if (conv_lr_ok(d)) { *path = 2; *ws = 0; return; }
     if (conv_hr_ok(d)) { *path = 1; *tile = conv_hr_tile(d); *ws = 0; }
   }
@@ -2089,7 +2063,7 @@ size_t pg_step_plan_workspace_size(const pg_step_plan* plan) { return plan ? pla
 
 int pg_step_plan_describe(const pg_step_plan* plan, char* buf, size_t len) {
   PG_CHECK_ARG(plan && buf && len > 0, "step_plan_describe: bad arguments");
-  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr", "conv_sk"};
+  static const char* path[] = {"conv3x3", "conv_hr", "conv_lr"};
   size_t o = 0;
   auto put = [&](const char* fmt, auto... a) {
     if (o < len) o += snprintf(buf + o, len - o, fmt, a...);

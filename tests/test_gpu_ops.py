@@ -980,67 +980,3 @@ def test_conv_rgbw_epilogue(B, H, C):
 def _lib_flag(name):
     from pggan_amd import _lib
     return getattr(_lib, name)
-
-
-SK_CASES = [
-    # (B, H, cin, cout, flags): the 4^2-16^2 convs of the step with the split-K workgroups and
-    # the in-launch combine (conv_sk.inc), incl. the mbstd conv's padded 513 -> 544 input
-    (4, 4, 512, 512, ("bias", "lrelu")),
-    (8, 4, 513, 512, ("bias", "lrelu")),
-    (4, 4, 512, 512, ("mask",)),
-    (4, 8, 512, 512, ("bias", "lrelu", "pool")),
-    (8, 8, 512, 512, ("mask", "accum")),
-    (4, 8, 512, 512, ("ups", "bias", "lrelu")),
-    (4, 16, 512, 512, ("bias", "lrelu", "pool")),
-    (8, 16, 512, 512, ("mask",)),
-    (4, 16, 512, 256, ("accum",)),
-]
-
-
-@pytest.mark.parametrize("case", SK_CASES)
-def test_conv_splitk_combine(case):
-    """bf16 convs at 4^2-16^2 through the split-K kernel with the fixed-order combine in the
-    launch (workspace + stream scratch given): against the CPU double, bitwise reproducible,
-    and within bf16 rounding of the single-slice path (no workspace)."""
-    B, H, cin, cout, fl = case
-    _L = lib()
-    dtype = torch.bfloat16
-    hip, cpu = ops_pair(dtype)
-    flags = 0
-    for f, v in (("ups", _L.CONV_UPS_IN), ("bias", _L.CONV_BIAS), ("lrelu", _L.CONV_LRELU),
-                 ("mask", _L.CONV_MASK), ("pool", _L.CONV_POOL), ("accum", _L.CONV_ACCUM)):
-        if f in fl:
-            flags |= v
-    Hin = H // 2 if "ups" in fl else H
-    xcs = cinp(cin)
-    x = q(rnd(B, Hin, Hin, xcs, seed=141), dtype)
-    x[..., cin:] = 0
-    w = rnd(cout, cin, 3, 3, seed=142)
-    bias = rnd(cout, seed=143) * 0.1
-    Ho = H // 2 if "pool" in fl else H
-    ycs = cout + 4
-    y0 = q(rnd(B, Ho, Ho, ycs, seed=144), dtype)
-    aux = q(rnd(B, H, H, cout, seed=145), dtype)
-    scale = 0.02
-    need = hip.conv_workspace_bytes(B=B, H=H, W=H, cin=cin, cout=cout)
-    assert need > 0, "the split-K kernel takes these shapes"
-    ws = torch.zeros((need + 3) // 4, dtype=torch.float32, device="cuda")
-    res = {}
-    for ops, dev in ((hip, "cuda"), (cpu, "cpu")):
-        dt = dtype if dev == "cuda" else torch.float32
-        wp = torch.zeros(ops.packed_elems(0, cout, cin), dtype=dt, device=dev)
-        ops.conv_pack(0, w.to(dev), scale, wp)
-        runs = [("sk", ws), ("sk2", ws), ("one", None)] if dev == "cuda" else [("ref", None)]
-        for name, wsp in runs:
-            y = y0.to(dev).to(dt).clone()
-            y2 = torch.zeros(B, H, H, cout, dtype=dt, device=dev) if "pool" in fl else None
-            ops.conv3x3(x.to(dev).to(dt), wp, y, B=B, H=H, W=H, cin=cin, cout=cout, flags=flags,
-                        slope=0.2, out_scale=0.25 if "pool" in fl else 1.0,
-                        bias=(bias * scale).to(dev), aux=aux.to(dev).to(dt), y2=y2, ws=wsp)
-            res[name] = (y, y2)
-    assert torch.equal(res["sk"][0], res["sk2"][0]), "split-K combine not bitwise reproducible"
-    for k in ("sk", "one"):
-        cmp(res[k][0], res["ref"][0], 2e-2, f"{k} y")
-        if res[k][1] is not None:
-            cmp(res[k][1], res["ref"][1], 2e-2, f"{k} y2")
-    cmp(res["sk"][0], res["one"][0].float().cpu(), 1e-2, "split vs single slice")
