@@ -1749,6 +1749,14 @@ int pg_linear_wgrad(int dtype, const pg_linear_desc* d, const void* x, const voi
   PG_CHECK_ARG(d && x && gy && dw, "linear_wgrad: bad args");
   const size_t n = (size_t)d->N * d->K;
   hipStream_t st = (hipStream_t)stream;
+  if (lin_fast_ok(dtype, d) && ((uintptr_t)dw & 15) == 0 && d->B <= LIN_MAXB && d->N % 8 == 0 &&
+      d->K % 1024 == 0) {
+    // bf16: 8 rows per workgroup over an LDS-staged x slice (coalesced dw streaming)
+    PG_KLAUNCH((lin_wgrad_rows<bf16_t, 8>), dim3((d->K + 1023) / 1024, d->N / 8), dim3(256), 0, st,
+                       *d, x, gy, dw, db);
+    PG_LAUNCH_CHECK();
+    return PG_OK;
+  }
   if (lin_fast_ok(dtype, d) && ((uintptr_t)dw & 15) == 0) {   // bf16: coalesced dw streaming
     PG_KLAUNCH(lin_wgrad_v<bf16_t>, dim3((d->K + 1023) / 1024, d->N), dim3(256), 0, st, *d, x,
                        gy, dw, db);
