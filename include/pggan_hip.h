@@ -100,6 +100,14 @@ size_t pg_scratch_bytes(void);
  * (img fp32 NCHW [B][3][H][W], summed over workgroups in a fixed order through `scratch`).
  * Only through pg_conv3x3_rgbw; query pg_conv3x3_supported. */
 #define PG_CONV_RGBW 4096
+/* fromRGB input gradient in the same epilogue (the penalty's input-gradient pass and the G
+ * half's, pggan/nets.py:255 backward): the conv result gz is not stored; instead
+ *   gimg[b][i] = f * sum_n W[n][i] gz[n]   (fp32 NCHW, written),
+ *   norms[b] += sum_pix sum_i gimg[b][i]^2 (if norms; the R1 / GP squared norms),
+ *   dw[n*3 + i] += s * sum_pix gz[n] gimg[i] (if dw; the R1 tangent's fromRGB weight term,
+ *                                             s = f / B: gbar = gimg / B)
+ * summed over workgroups in a fixed order through `scratch`.  Only through pg_conv3x3_rgbd. */
+#define PG_CONV_RGBD 8192
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -151,6 +159,14 @@ int pg_conv3x3_fwd_ex(int dtype, const pg_conv_desc* d, const void* x, const voi
 int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                     const void* aux, const float* img, float s, float* dw, float* db,
                     void* scratch, void* stream);
+/* The input-gradient conv of PG_CONV_RGBD (d->flags includes it, y not written, B <= 16): x,
+ * wpk, aux as pg_conv3x3_fwd; w_rgb [C][3] the fromRGB weights, f their He constant; gimg the
+ * image gradient written; norms [B] accumulated or NULL; dw [C*3] accumulated or NULL with
+ * scale s; scratch a PG_SCRATCH_BYTES reduction scratch of the stream.  Replaces
+ * pg_conv3x3_fwd + pg_from_rgb_bwd(gimg, norms) (+ the tangent's pg_from_rgb_bwd(dw)). */
+int pg_conv3x3_rgbd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const void* aux, const float* w_rgb, float f, float* gimg, float* norms,
+                    float* dw, float s, void* scratch, void* stream);
 /* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
  * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);

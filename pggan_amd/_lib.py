@@ -19,6 +19,7 @@ CONV_UPS_IN, CONV_BIAS, CONV_LRELU, CONV_MASK, CONV_POOL, CONV_ACCUM = 1, 2, 4, 
 CONV_PIXNORM = 64
 CONV_PNBWD = 2048
 CONV_RGBW = 4096
+CONV_RGBD = 8192
 CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
@@ -99,6 +100,8 @@ _SIGS = {
     "pg_conv3x3_supported": ([_I, ctypes.POINTER(ConvDesc), _SZ], _I),
     "pg_conv3x3_rgbw": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _VP],
                         _I),
+    "pg_conv3x3_rgbd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _F,
+                         _VP, _VP], _I),
     "pg_conv3x3_fwd_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                            _SZ, _VP], _I),
     "pg_conv3x3_wgrad_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _F, _VP, _VP, _VP, _SZ,
@@ -420,6 +423,20 @@ class HipOps:
                                            _p(img), float(s), _p(dw), _p(db),
                                            self._scr(), self._s()),
                   "conv3x3_rgbw")
+
+    def conv3x3_rgbd(self, x, wpk, *, B, H, W, cin, cout, flags, aux, w_rgb, f, gimg,
+                     norms=None, dw=None, s=0.0, slope=0.2, out_scale=1.0):
+        """The input-gradient conv whose result is the fromRGB output's gradient gz, with the
+        fromRGB input gradient gimg = f W^T gz (written), the per-sample squared norms of gimg
+        (norms, accumulated) and s * sum gz (x) gimg (dw, accumulated) in its epilogue instead of
+        storing gz (include/pggan_hip.h: PG_CONV_RGBD)."""
+        self._cuda(x, wpk, aux, w_rgb, gimg, norms, dw)
+        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], cout, aux.shape[-1], 0,
+                     flags | CONV_RGBD, slope, out_scale, 0)
+        self._chk(self.lib.pg_conv3x3_rgbd(self._dt(x), ctypes.byref(d), _p(x), _p(wpk), _p(aux),
+                                           _p(w_rgb), float(f), _p(gimg), _p(norms), _p(dw),
+                                           float(s), self._scr(), self._s()),
+                  "conv3x3_rgbd")
 
     def conv_supported(self, *, B, H, W, cin, cout, flags, ws_bytes=0):
         """Whether the conv kernel picked for this shape supports `flags` (fused epilogues)."""

@@ -56,6 +56,11 @@ struct ConvParams {
   float* rdb;         // [cout], accumulated
   float* scratch;     // det_commit scratch of the stream
   float rscale;
+  // PG_CONV_RGBD: fromRGB input gradient of the conv result
+  const float* rw;    // fromRGB weights [cout][3]
+  float* gimg;        // fp32 NCHW [B][3][H][W], written
+  float* norms;       // [B] per-sample squared norms, accumulated (or NULL)
+  float f2;           // gimg = f2 * W^T gz
 };
 
 // the RGBW operands of the next conv_hr launch on this host thread (pg_conv3x3_rgbw)
@@ -65,6 +70,11 @@ struct RgbwArgs {
   float* db = nullptr;
   float* scratch = nullptr;
   float s = 0.f;
+  // RGBD
+  const float* rw = nullptr;
+  float* gimg = nullptr;
+  float* norms = nullptr;
+  float f = 0.f;
 };
 static thread_local RgbwArgs g_rgbw;
 
@@ -1704,9 +1714,12 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
-  if (d->flags & PG_CONV_RGBW) {   // the EF tiles 0 / 5 (16 / 32 channels, H >= 512 here)
+  if (d->flags & (PG_CONV_RGBW | PG_CONV_RGBD)) {   // the EF tiles 0 / 5 (16 / 32 channels)
     if constexpr (sizeof(T) != 2) return false;
-    if (d->flags != (PG_CONV_RGBW | PG_CONV_MASK | PG_CONV_AUX_BITS) || !conv_hr_ok(d)) return false;
+    const int rf = d->flags & (PG_CONV_RGBW | PG_CONV_RGBD);
+    if (rf == (PG_CONV_RGBW | PG_CONV_RGBD)) return false;
+    if (d->flags != (rf | PG_CONV_MASK | PG_CONV_AUX_BITS) || !conv_hr_ok(d)) return false;
+    if ((d->flags & PG_CONV_RGBD) && d->B > 16) return false;
     const int t = conv_hr_tile(d);
     return (t == 0 && d->cout == 16) || (t == 5 && d->cout == 32);
   }
@@ -1880,6 +1893,25 @@ int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void*
                "conv3x3_rgbw: bad channel strides");
   PG_CHECK_ARG(pg_det_fits((size_t)256 * 8, (size_t)d->cout * 4), "conv3x3_rgbw: scratch too small");
   g_rgbw.img = img; g_rgbw.dw = dw; g_rgbw.db = db; g_rgbw.scratch = (float*)scratch; g_rgbw.s = s;
+  const int rc = conv_dispatch<bf16_t>(d, x, wpk, nullptr, aux, nullptr, nullptr, nullptr, 0,
+                                       (hipStream_t)stream);
+  g_rgbw = RgbwArgs{};
+  return rc;
+}
+
+int pg_conv3x3_rgbd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const void* aux, const float* w_rgb, float f, float* gimg, float* norms,
+                    float* dw, float s, void* scratch, void* stream) {
+  PG_CHECK_ARG(d && x && wpk && aux && w_rgb && gimg && scratch, "conv3x3_rgbd: null pointer");
+  PG_CHECK_ARG(dtype == PG_BF16 && (d->flags & PG_CONV_RGBD) && conv_supported<bf16_t>(d, 0),
+               "conv3x3_rgbd: flags 0x%x not supported for %d -> %d at %dx%d (B %d)", d->flags,
+               d->cin, d->cout, d->H, d->W, d->B);
+  PG_CHECK_ARG(d->x_cs >= cinp_of(d->cin) && d->x_cs % 8 == 0 && d->aux_cs * 8 >= d->cout,
+               "conv3x3_rgbd: bad channel strides");
+  PG_CHECK_ARG(pg_det_fits((size_t)256 * 8, (size_t)16 + d->cout * 4), "conv3x3_rgbd: scratch too small");
+  g_rgbw = RgbwArgs{};
+  g_rgbw.rw = w_rgb; g_rgbw.f = f; g_rgbw.gimg = gimg; g_rgbw.norms = norms; g_rgbw.dw = dw;
+  g_rgbw.s = s; g_rgbw.scratch = (float*)scratch;
   const int rc = conv_dispatch<bf16_t>(d, x, wpk, nullptr, aux, nullptr, nullptr, nullptr, 0,
                                        (hipStream_t)stream);
   g_rgbw = RgbwArgs{};

@@ -192,6 +192,7 @@ ENGINE_DEFAULTS = dict(
     tail_main=True,        # the last weight gradients of a final pass on the main stream
     sep_b2=True,           # the merged second backward writes its own gradient buffers
     fuse_rgbw=True,        # the final pass's fromRGB weight gradient in the top conv's epilogue
+    fuse_rgbd=True,        # the fromRGB input gradient (+ norms, + R1 tangent term) there too
 )
 
 
@@ -732,6 +733,22 @@ class StepEngine:
             self._ws_cache[key] = ok
         return self._ws_cache[key]
 
+    def _rgbd(self):
+        """Whether the input-gradient passes (the penalty's B1, the G half's) compute the top
+        fromRGB input gradient, its squared norms and (R1) the tangent's fromRGB weight term in
+        the epilogue of the top conv a's input gradient (PG_CONV_RGBD: that gradient is never
+        written)."""
+        key = ("rgbd", 0, 0, 0, 0)
+        if key not in self._ws_cache:
+            f = self._conv_sup()
+            d, s, R, B = self.depths, self.s, self.R, self.B
+            ok = bool(self.fuse_rgbd and self._rgbbits() and hasattr(self.ops, "conv3x3_rgbd") and
+                      B <= 16 and
+                      f(B=B, H=R, W=R, cin=d[s], cout=d[s],
+                        flags=L.CONV_MASK | L.CONV_AUX_BITS | L.CONV_RGBD))
+            self._ws_cache[key] = ok
+        return self._ws_cache[key]
+
     def _pn_pool(self, i):
         """Whether level i's conv-a input gradient (pooled to level i-1) also applies level
         i-1's conv-b PixelNorm + LReLU backward (PG_CONV_POOL | PG_CONV_PNBWD): level i-1's
@@ -998,7 +1015,7 @@ class StepEngine:
             self.grad_ready(net, names)
 
     def d_backward(self, P, GR, u, alpha, img=None, gimg=None, inj_mbstd=None, final=False,
-                   gimg_overwrite=False, norms=None, join=True):
+                   gimg_overwrite=False, norms=None, join=True, t_dw=None):
         """Backward from u = dL/dlogit.  GR: grad views (None -> input-gradient only);
         gimg: accumulate dL/dimg (zeroed by the caller unless gimg_overwrite: the first
         fromRGB input gradient then writes it); norms: += per-sample sum of dL/dimg^2, fused
@@ -1018,6 +1035,12 @@ class StepEngine:
         fr = "fromRGB_blocks.{}.fromRGB.module."
         rgbw = (tail and gimg is None and s >= 1 and isinstance(img, torch.Tensor) and
                 self._rgbw())
+        # the input-gradient passes: gimg (+ norms, + the R1 tangent's fromRGB weight term
+        # t_dw, s / B) from the top conv a's epilogue (t_dw only without the fade-in branch,
+        # whose gradient joins gimg afterwards)
+        rgbd = (GR is None and gimg is not None and gimg_overwrite and s >= 1 and self._rgbd())
+        low_a = self._low(alpha)
+        self._t_rgb_done = bool(rgbd and t_dw is not None and not low_a)
         ready = (lambda *p: self._ready("D", *p)) if final else (lambda *p: None)
         dec = "decision_layer.module."
         lin = "minibatch_normalization_block.linear.module."
@@ -1084,7 +1107,14 @@ class StepEngine:
                             d[i + 1],
                             db=GR[a + "bias"])
                 ready(a)
-            if i == s - 1 and rgbw:
+            if i == s - 1 and rgbd:
+                fw = fr.format(s) + "weight"
+                ops.conv3x3_rgbd(D[f"gza{i}"], self.packs[("D", f"a{i}")][1], B=B, H=Ri, W=Ri,
+                                 cin=d[i + 1], cout=d[i + 1], flags=L.CONV_MASK | L.CONV_AUX_BITS,
+                                 slope=SLOPE, aux=D["rgbb"], w_rgb=P[fw], f=he(3), gimg=gimg,
+                                 norms=None if low_a else norms,
+                                 dw=t_dw if self._t_rgb_done else None, s=he(3) / B)
+            elif i == s - 1 and rgbw:
                 # the fromRGB weight gradient in this conv's epilogue: its result is not stored
                 self._tail_wait()   # after the tangent's fromRGB weight term (side stream)
                 fw = fr.format(s)
@@ -1127,7 +1157,7 @@ class StepEngine:
                             D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, img=img,
                             dw=GR[fr.format(s) + "weight"], db=GR[fr.format(s) + "bias"])
             ready(fr.format(s))
-        if gimg is not None:
+        if gimg is not None and not rgbd:
             ops.from_rgb_bwd(D["gzrgb"], w, he(3), B=B, R=R, C=d[s], down=False, gimg=gimg,
                              **self._gimg_kw(gimg_overwrite, None if low else norms))
         if low:
@@ -1156,13 +1186,17 @@ class StepEngine:
         gradient read by the tangent pass through an image mix (the ops support it)."""
         return hasattr(self.ops, "penalty_scale")
 
-    def _input_grad(self, P, u, alpha, mode, w=0.0):
+    def _input_grad(self, P, u, alpha, mode, w=0.0, GR=None):
         """B1 of a penalty: dD/dx into D["gimg"] from the upstream u, the penalty into
-        loss[2] and the tangent pass's input gbar (R1: g / B; WGAN-GP: the weighted g)."""
+        loss[2] and the tangent pass's input gbar (R1: g / B; WGAN-GP: the weighted g).
+        GR (R1): the D gradients, so the tangent's fromRGB weight term can be taken in this
+        pass (PG_CONV_RGBD; d_tangent then skips it)."""
         ops, D, B = self.ops, self.dd, self.B
         if self._fused_penalty():
+            fw = f"fromRGB_blocks.{self.s}.fromRGB.module.weight"
             self.d_backward(P, None, u, alpha, gimg=D["gimg"], gimg_overwrite=True,
-                            norms=D["gp_norms"])
+                            norms=D["gp_norms"],
+                            t_dw=GR[fw] if (GR is not None and mode == "r1") else None)
             ops.penalty_scale(mode, D["gp_norms"], w, self.loss[2:3], D["gp_scale"])
             return L.ImgMix(D["gimg"], a=D["gp_scale"])
         D["gimg"].zero_()
@@ -1182,9 +1216,11 @@ class StepEngine:
         mk = dict(mask_bits=D["rgbb"]) if self._rgbbits() else dict(mask_y=D["yrgb"])
         ops.from_rgb(gbar, P[fr.format(s) + "weight"], None, he(3), D["trgb"], B=B, R=R, C=d[s],
                      down=False, slope=SLOPE, **mk)
-        self._side_call(("D",), ops.from_rgb_bwd,
-                        D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
-                        down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
+        if not getattr(self, "_t_rgb_done", False):   # else B1's RGBD epilogue added it
+            self._side_call(("D",), ops.from_rgb_bwd,
+                            D["gzrgb"], P[fr.format(s) + "weight"], he(3), B=B, R=R, C=d[s],
+                            down=False, img=gbar, dw=GR[fr.format(s) + "weight"])
+        self._t_rgb_done = False
         low = self._low(alpha)
         if low:
             ops.from_rgb(gbar, P[fr.format(s - 1) + "weight"], None, he(3), D["td"], B=B, R=R // 2,
@@ -1264,7 +1300,7 @@ class StepEngine:
             # ---- real: F, B1, R1, T, B2
             self.d_forward(PD, xr, alpha_D)
             ops.bce(D["logit"], True, 1.0, self.loss[0:1], D["u"], D["hl"])   # lib/loss.py:119-123
-            gbar = self._input_grad(PD, D["u"], alpha_D, "r1")                # lib/loss.py:125-135
+            gbar = self._input_grad(PD, D["u"], alpha_D, "r1", GR=GD)          # lib/loss.py:125-135
             tout, inj = self.d_tangent(PD, GD, gbar, D["u"], alpha_D)
             ops.mul_add(D["u"], tout.view(-1), D["hl"], D["u2"])
             self.d_backward(PD, GD, D["u2"], alpha_D, img=xr, inj_mbstd=inj)
@@ -1368,7 +1404,7 @@ class StepEngine:
             return X[:B], (img_fake.clone() if self.keep_fake_D else img_fake)
         ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], D1["hl"])    # lib/loss.py:119-123
         ops.bce(D2["logit"][B:], False, 1.0, self.loss[1:2], D2["u2"][B:], None)
-        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1")                     # lib/loss.py:125-135
+        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1", GR=GD)              # lib/loss.py:125-135
         tout, inj = self.d_tangent(PD, GD, gbar, D1["u"], alpha_D)
         ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
         self.h_mb = h2
@@ -1431,7 +1467,7 @@ class StepEngine:
             self._copy(X[:B], real)
         self.d_forward(PD, X[:B], alpha_D)                                       # :216
         ops.bce(D1["logit"], True, 1.0, self.loss[0:1], D1["u"], D1["hl"])    # lib/loss.py:119-123
-        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1")                     # lib/loss.py:125-135
+        gbar = self._input_grad(PD, D1["u"], alpha_D, "r1", GR=GD)              # lib/loss.py:125-135
         tout, inj = self.d_tangent(PD, GD, gbar, D1["u"], alpha_D)
         ops.mul_add(D1["u"], tout.view(-1), D1["hl"], D1["u2"])
         if before_fake is not None:

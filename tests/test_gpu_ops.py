@@ -980,3 +980,42 @@ def test_conv_rgbw_epilogue(B, H, C):
 def _lib_flag(name):
     from pggan_amd import _lib
     return getattr(_lib, name)
+
+
+@pytest.mark.parametrize("B,H,C", [(4, 1024, 16), (2, 512, 32), (3, 512, 32)])
+def test_conv_rgbd_epilogue(B, H, C):
+    """PG_CONV_RGBD (bf16): the top conv a's input gradient with the fromRGB input gradient
+    gimg = f W^T gz (written), its per-sample squared norms (accumulated) and the R1 tangent's
+    fromRGB weight term s sum gz (x) gimg (accumulated) in its epilogue, against the same conv
+    on the CPU double followed by float64 arithmetic; bitwise reproducible."""
+    from cpu_ops import CONV_AUX_BITS, CONV_MASK
+    hip, cpu = ops_pair(torch.bfloat16)
+    fl = CONV_MASK | CONV_AUX_BITS
+    assert hip.conv_supported(B=B, H=H, W=H, cin=C, cout=C, flags=fl | _lib_flag("CONV_RGBD"))
+    dt = torch.bfloat16
+    x = q(rnd(B, H, H, C, seed=151), dt)
+    wd = q(rnd(r16(C) * 9 * cinp(C), seed=152, scale=0.05), dt)
+    bits = torch.randint(0, 256, (B, H, H, C // 8), dtype=torch.uint8,
+                         generator=torch.Generator().manual_seed(153))
+    wr = rnd(C, 3, seed=154)
+    f, s = 0.8165, 0.8165 / B
+    n0, dw0 = rnd(B, seed=155).abs(), rnd(C * 3, seed=156)
+    gz = torch.zeros(B, H, H, C)
+    cpu.conv3x3(x.float(), wd.float(), gz, B=B, H=H, W=H, cin=C, cout=C, flags=fl, aux=bits)
+    g64 = gz.double()
+    gimg_ref = f * torch.einsum("bhwn,ni->bihw", g64, wr.double())
+    norms_ref = n0.double() + (gimg_ref ** 2).sum(dim=(1, 2, 3))
+    dw_ref = dw0.double().view(C, 3) + s * torch.einsum("bhwn,bihw->ni", g64, gimg_ref)
+    outs = []
+    for _ in range(2):
+        gimg = torch.full((B, 3, H, H), float("nan"), device="cuda")
+        norms, dw = n0.clone().cuda(), dw0.clone().cuda()
+        hip.conv3x3_rgbd(x.to(dt).cuda(), wd.to(dt).cuda(), B=B, H=H, W=H, cin=C, cout=C, flags=fl,
+                         aux=bits.cuda(), w_rgb=wr.cuda(), f=f, gimg=gimg, norms=norms, dw=dw, s=s)
+        outs.append((gimg.cpu(), norms.cpu(), dw.cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b), "RGBD outputs not bitwise reproducible"
+    for got, ref, what in ((outs[0][0], gimg_ref, "gimg"), (outs[0][1], norms_ref, "norms"),
+                           (outs[0][2].view(C, 3), dw_ref, "dw")):
+        err = float((got.double() - ref).norm() / ref.norm())
+        assert err <= 1e-4, (what, err)
