@@ -237,6 +237,12 @@ int pg_rgb_out_bwd(int dtype, int B, int R, int C, int x_cs, const void* x, cons
 int pg_rgb_out_bwd_pn(int dtype, int B, int R, int C, int y_cs, const void* y, const float* r,
                       const float* w, float c, const float* gimg, float slope, int gz_cs, void* gz,
                       void* stream);
+/* pg_rgb_out_bwd_pn with the toRGB weight / bias gradients of the same pass (dw[i][k] +=
+ * c sum gimg[i] y[k], db[i] += c sum gimg[i]; scratch: the stream's PG_SCRATCH_BYTES reduction
+ * scratch): y and gimg are streamed once for both (lib/blocks.py toRGB, pggan/nets.py:140-156) */
+int pg_rgb_out_bwd_pn_wg(int dtype, int B, int R, int C, int y_cs, const void* y, const float* r,
+                         const float* w, float c, const float* gimg, float slope, int gz_cs,
+                         void* gz, float* dw, float* db, void* scratch, void* stream);
 int pg_from_rgb(int dtype, int B, int R, int C, const float* img, int down, const float* w,
                 const float* b, float c, float slope, const void* mask_y, int y_cs, void* y,
                 void* stream);

@@ -127,6 +127,8 @@ _SIGS = {
     "pg_from_rgb_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP, _I,
                          _VP, _VP], _I),
     "pg_rgb_out_bwd_pn": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _F, _I, _VP, _VP], _I),
+    "pg_rgb_out_bwd_pn_wg": ([_I, _I, _I, _I, _I, _VP, _VP, _VP, _F, _VP, _F, _I, _VP, _VP, _VP,
+                              _VP, _VP], _I),
     "pg_from_rgb_bits": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _VP, _F, _F, _VP,
                           _I, _VP, _VP, _VP], _I),
     "pg_from_rgb_bwd_src": ([_I, _I, _I, _I, ctypes.POINTER(ImgSrcDesc), _I, _VP, _F, _I, _VP, _VP,
@@ -537,8 +539,16 @@ class HipOps:
                                           alpha, _p(gimg), _p(gx), _p(gxp), _p(dw), _p(db), _p(dwp),
                                           _p(dbp), self._scr(), self._s()), "rgb_out_bwd")
 
-    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope):
-        """toRGB input gradient + the PixelNorm / LReLU backward of its input y (pg_rgb_out_bwd_pn)."""
+    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope, dw=None, db=None):
+        """toRGB input gradient + the PixelNorm / LReLU backward of its input y (pg_rgb_out_bwd_pn);
+        with dw / db also the toRGB weight / bias gradients of the same pass (_wg)."""
+        if dw is not None:
+            self._cuda(y, r, w, gimg, gz, dw, db)
+            self._chk(self.lib.pg_rgb_out_bwd_pn_wg(self._dt(y), B, R, C, y.shape[-1], _p(y), _p(r),
+                                                    _p(w), c, _p(gimg), slope, gz.shape[-1], _p(gz),
+                                                    _p(dw), _p(db), self._scr(), self._s()),
+                      "rgb_out_bwd_pn_wg")
+            return
         self._cuda(y, r, w, gimg, gz)
         self._chk(self.lib.pg_rgb_out_bwd_pn(self._dt(y), B, R, C, y.shape[-1], _p(y), _p(r), _p(w), c,
                                              _p(gimg), slope, gz.shape[-1], _p(gz), self._s()),

@@ -1525,6 +1525,22 @@ int pg_rgb_out_bwd_pn(int dtype, int B, int R, int C, int y_cs, const void* y, c
   return PG_OK;
 }
 
+int pg_rgb_out_bwd_pn_wg(int dtype, int B, int R, int C, int y_cs, const void* y, const float* r,
+                         const float* w, float c, const float* gimg, float slope, int gz_cs,
+                         void* gz, float* dw, float* db, void* scratch, void* stream) {
+  PG_CHECK_ARG(y && r && w && gimg && gz && dw && scratch && (C == 16 || C == 32),
+               "rgb_out_bwd_pn_wg: bad args (C 16 / 32)");
+  hipStream_t st = (hipStream_t)stream;
+  const int rc = dtype == PG_F32
+                     ? try_rgb_dgrad_pn<float>(B, R, C, y_cs, (const float*)y, r, w, c, slope, gimg,
+                                               gz_cs, (float*)gz, st, dw, db, (float*)scratch)
+                     : try_rgb_dgrad_pn<bf16_t>(B, R, C, y_cs, (const bf16_t*)y, r, w, c, slope, gimg,
+                                                gz_cs, (bf16_t*)gz, st, dw, db, (float*)scratch);
+  PG_CHECK_ARG(rc == 0, "rgb_out_bwd_pn_wg: unsupported strides (%d, %d)", y_cs, gz_cs);
+  PG_LAUNCH_CHECK();
+  return PG_OK;
+}
+
 static int from_rgb_impl(int dtype, int B, int R, int C, const ImgSrc& img, int down,
                          const float* w, const float* b, float c, float slope, const void* mask_y,
                          int y_cs, void* y, hipStream_t st) {

@@ -193,6 +193,7 @@ ENGINE_DEFAULTS = dict(
     sep_b2=True,           # the merged second backward writes its own gradient buffers
     fuse_rgbw=True,        # the final pass's fromRGB weight gradient in the top conv's epilogue
     fuse_rgbd=True,        # the fromRGB input gradient (+ norms, + R1 tangent term) there too
+    fuse_torgb_wg=True,    # the toRGB weight gradient in the toRGB input-gradient pass
 )
 
 
@@ -878,18 +879,25 @@ class StepEngine:
                   self.fuse_rgb_pnbwd and
                   self._pn_fused(self.R, d[s], d[s], L.CONV_LRELU))
         w_rgb = P[pre + "weight"]
+        # the toRGB weight gradient in the same pass as the input gradient where the fused form
+        # runs (y and gimg streamed once, on the main stream: rgb_dgrad_pn_wg_v)
+        wg_fused = top_pn and self.fuse_torgb_wg
         if top_pn:
             ops.rgb_out_bwd_pn(self._ylvl(s), g[f"rb{s - 1}"], w_rgb, he(d[s]), gimg,
-                               g[f"gzb{s - 1}"], B=B, R=self.R, C=d[s], slope=SLOPE)
+                               g[f"gzb{s - 1}"], B=B, R=self.R, C=d[s], slope=SLOPE,
+                               **(dict(dw=GR[pre + "weight"], db=GR[pre + "bias"]) if wg_fused else {}))
         else:
             ops.rgb_out_bwd(self._ylvl(s), w_rgb, he(d[s]), gimg, g[f"gy{s}"], None, None,
                             B=B, R=self.R, C=d[s],
                             **{k: (None if k in ("dwp", "dbp") else v) for k, v in kw.items()})
-        # img / the fade-in branch's operands are D / G buffers: pending for both nets
-        self._side_call(("G", "D"), ops.rgb_out_bwd, self._ylvl(s), w_rgb, he(d[s]), gimg, None,
-                        GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s],
-                        **{k: (None if k == "gxp" else v) for k, v in kw.items()})
-        self._ready("G", pre, *([f"toRGB_blocks.{s - 1}.toRGB.module."] if s >= 1 else []))
+        if wg_fused:
+            self._ready_main("G", pre)
+        else:
+            # img / the fade-in branch's operands are D / G buffers: pending for both nets
+            self._side_call(("G", "D"), ops.rgb_out_bwd, self._ylvl(s), w_rgb, he(d[s]), gimg, None,
+                            GR[pre + "weight"], GR[pre + "bias"], B=B, R=self.R, C=d[s],
+                            **{k: (None if k == "gxp" else v) for k, v in kw.items()})
+            self._ready("G", pre, *([f"toRGB_blocks.{s - 1}.toRGB.module."] if s >= 1 else []))
         pn_done = s - 1 if top_pn else None   # level whose conv-b PixelNorm backward is done
         for i in reversed(range(s)):
             Ri = 8 * 2 ** i

@@ -233,9 +233,11 @@ class CpuOps:
             if dbp is not None:
                 dbp.add_(fp * gs.reshape(-1, 3).sum(0))
 
-    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope):
+    def rgb_out_bwd_pn(self, y, r, w, c, gimg, gz, *, B, R, C, slope, dw=None, db=None):
         gy = torch.zeros_like(y)
         gy[..., :C] = c * gimg.permute(0, 2, 3, 1) @ w.view(3, C)
+        if dw is not None:
+            self.rgb_out_bwd(y, w, c, gimg, None, dw, db, B=B, R=R, C=C)
         self.pixnorm_lrelu_bwd_y(y, r, gy, gz, C, slope)
 
     def _img_in(self, img, down):

@@ -766,6 +766,16 @@ def test_rgb_out_bwd_pn(dtype, C, R):
             gz2 = torch.zeros_like(gz)
             ops.pixnorm_lrelu_bwd_y(Y, Rr, gy, gz2, C, 0.2)
             cmp(gz, gz2.cpu(), tol_for(dtype, 1e-6), "fused vs unfused")
+            # with the toRGB weight / bias gradients in the same pass (_wg): the same gz, and the
+            # gradients of the separate pass (accumulated onto existing values)
+            dw0, db0 = rnd(3 * C, seed=115).to(dev), rnd(3, seed=116).to(dev)
+            gz3, dw, db = torch.zeros_like(gz), dw0.clone(), db0.clone()
+            ops.rgb_out_bwd_pn(Y, Rr, Wd, 0.35, G, gz3, B=B, R=R, C=C, slope=0.2, dw=dw, db=db)
+            assert torch.equal(gz3, gz)
+            dw2, db2 = dw0.clone(), db0.clone()
+            ops.rgb_out_bwd(Y, Wd, 0.35, G, None, dw2, db2, B=B, R=R, C=C)
+            cmp(dw, (dw2 - dw0).cpu() + dw0.cpu(), 1e-5, "toRGB dw fused")
+            cmp(db, (db2 - db0).cpu() + db0.cpu(), 1e-5, "toRGB db fused")
     cmp(res["cuda"], res["cpu"], tol_for(dtype, 1e-6), f"gz C={C} R={R}")
 
 
