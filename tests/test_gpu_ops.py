@@ -446,6 +446,11 @@ WIDE_CASES = [
     (2, 512, 64, 32, ("ups", "bias", "lrelu", "pixnorm")),
     # the 32^2 wide convs of the merged passes (B = 8) on the 16-row tile
     (8, 32, 512, 512, ("bias", "lrelu")),
+    # tile 16 (64 -> 64, CK = 64, persistent, compile-time flags): the 256^2 level
+    (4, 256, 64, 64, ()),
+    (8, 256, 64, 64, ("mask",)),
+    (8, 256, 64, 64, ("bias", "lrelu")),
+    (2, 128, 64, 64, ("bias", "lrelu", "pixnorm")),
 ]
 
 
