@@ -194,6 +194,7 @@ ENGINE_DEFAULTS = dict(
     fuse_rgbw=True,        # the final pass's fromRGB weight gradient in the top conv's epilogue
     fuse_rgbd=True,        # the fromRGB input gradient (+ norms, + R1 tangent term) there too
     fuse_torgb_wg=True,    # the toRGB weight gradient in the toRGB input-gradient pass
+    tail_b=True,           # ... with tail_main: the top level's conv-b weight gradient too
 )
 
 
@@ -1086,11 +1087,15 @@ class StepEngine:
                 ops.unpool_mask(g, D["yd"], D["gzd"], B=B, H=Ri // 2, W=Ri // 2, C=d[i],
                                 scale=1.0 - alpha, slope=SLOPE, ups=False)
             sc = 0.25 * (alpha if i == s - 1 else 1.0)
+            # the final pass's top conv-b weight gradient on the main stream after conv a's
+            # (tail_b): the side stream's queue is the step's critical path at this point
+            tail_b = tail and i == s - 1 and self.tail_b
             if self._dbits(i):
                 # gzb = sc * up2(g) * lrelu'(bits): read by the kernels from g and the bits
-                if GR is not None:
+                wgb = dict(db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc) if GR is not None else None
+                if GR is not None and not tail_b:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
-                                db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc)
+                                **wgb)
                     ready(b)
                 self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
@@ -1102,9 +1107,10 @@ class StepEngine:
                 else:
                     ops.unpool_mask(g, D[f"bf{i}"], D[f"gzb{i}"], B=B, H=Ri, W=Ri, C=d[i], scale=sc,
                                     slope=SLOPE, ups=True)
-                if GR is not None:
+                wgb = dict(db=GR[b + "bias"]) if GR is not None else None
+                if GR is not None and not tail_b:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
-                                d[i + 1], d[i], db=GR[b + "bias"])
+                                d[i + 1], d[i], **wgb)
                     ready(b)
                 self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
@@ -1147,6 +1153,10 @@ class StepEngine:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
                             d[i + 1], db=GR[a + "bias"], main=True)
                 self._ready_main("D", a)
+                if tail_b:
+                    self._wgrad("D", f"b{i}", D[f"a{i}"], g if self._dbits(i) else D[f"gzb{i}"],
+                                GR[b + "weight"], Ri, d[i + 1], d[i], main=True, **wgb)
+                    self._ready_main("D", b)
         if s == 0:
             ops.unpool_mask(D["gh"], D["yrgb"], D["gzrgb"], B=B, H=4, W=4, C=d[0], scale=1.0,
                             slope=SLOPE, ups=False)
