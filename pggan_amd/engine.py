@@ -195,6 +195,7 @@ ENGINE_DEFAULTS = dict(
     fuse_rgbd=True,        # the fromRGB input gradient (+ norms, + R1 tangent term) there too
     fuse_torgb_wg=True,    # the toRGB weight gradient in the toRGB input-gradient pass
     tail_b=True,           # ... with tail_main: the top level's conv-b weight gradient too
+    tail_levels=1,         # ... and both weight gradients of this many top levels
 )
 
 
@@ -1079,6 +1080,7 @@ class StepEngine:
             ops.blend(1.0, D["gh"], 1.0, inj_mbstd, D["gh"])
         g = D["gh"]
         low = self._low(alpha)
+        tail_jobs = []   # (order, _wgrad args, kwargs, grad_ready prefix) run at the tail
         for i in range(s):
             Ri = 8 * 2 ** i
             a, b = f"blocks.{i}.block.0.module.", f"blocks.{i}.block.2.module."
@@ -1087,9 +1089,11 @@ class StepEngine:
                 ops.unpool_mask(g, D["yd"], D["gzd"], B=B, H=Ri // 2, W=Ri // 2, C=d[i],
                                 scale=1.0 - alpha, slope=SLOPE, ups=False)
             sc = 0.25 * (alpha if i == s - 1 else 1.0)
-            # the final pass's top conv-b weight gradient on the main stream after conv a's
-            # (tail_b): the side stream's queue is the step's critical path at this point
-            tail_b = tail and i == s - 1 and self.tail_b
+            # the final pass's top-level weight gradients on the main stream after its
+            # input-gradient chain (tail_main / tail_b / tail_levels): the side stream's queue
+            # is the step's critical path at this point
+            in_tail = tail and i >= s - max(1, self.tail_levels)
+            tail_b = in_tail and (i < s - 1 or self.tail_b)
             if self._dbits(i):
                 # gzb = sc * up2(g) * lrelu'(bits): read by the kernels from g and the bits
                 wgb = dict(db=GR[b + "bias"], gzbits=D[f"mb{i}"], gscale=sc) if GR is not None else None
@@ -1097,6 +1101,9 @@ class StepEngine:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri, d[i + 1], d[i],
                                 **wgb)
                     ready(b)
+                elif tail_b:
+                    tail_jobs.append(((-i, 1), (f"b{i}", D[f"a{i}"], g, GR[b + "weight"], Ri,
+                                                d[i + 1], d[i]), wgb, b))
                 self._conv("D", f"b{i}", g, D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK | L.CONV_UPS_IN | L.CONV_X_BITS, aux=D[f"a{i}"],
                            dgrad=True, out_scale=sc, xbits=D[f"mb{i}"])
@@ -1112,15 +1119,21 @@ class StepEngine:
                     self._wgrad("D", f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"], Ri,
                                 d[i + 1], d[i], **wgb)
                     ready(b)
+                elif tail_b:
+                    tail_jobs.append(((-i, 1), (f"b{i}", D[f"a{i}"], D[f"gzb{i}"], GR[b + "weight"],
+                                                Ri, d[i + 1], d[i]), wgb, b))
                 self._conv("D", f"b{i}", D[f"gzb{i}"], D[f"gza{i}"], Ri, d[i], d[i + 1],
                            L.CONV_MASK, aux=D[f"a{i}"], dgrad=True)
             hin = D["yrgb"] if i == s - 1 else (self._top_out(alpha) if i == s - 2 else D[f"p{i + 1}"])
             top_tail = tail and i == s - 1
-            if GR is not None and not top_tail:
+            if GR is not None and not in_tail:
                 self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
                             d[i + 1],
                             db=GR[a + "bias"])
                 ready(a)
+            elif in_tail:
+                tail_jobs.append(((-i, 0), (f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri,
+                                            d[i + 1], d[i + 1]), dict(db=GR[a + "bias"]), a))
             if i == s - 1 and rgbd:
                 fw = fr.format(s) + "weight"
                 ops.conv3x3_rgbd(D[f"gza{i}"], self.packs[("D", f"a{i}")][1], B=B, H=Ri, W=Ri,
@@ -1147,16 +1160,13 @@ class StepEngine:
                            dgrad=True)
                 g = D[f"ghin{i}"]
             if top_tail:
-                # the input-gradient chain ends here: this weight gradient on the main stream
-                # (idle otherwise) while the side stream drains its queue
+                # the input-gradient chain ends here: the deferred weight gradients on the main
+                # stream (idle otherwise) while the side stream drains its queue, the top
+                # level's first, conv a before conv b
                 self._tail_wait()
-                self._wgrad("D", f"a{i}", hin, D[f"gza{i}"], GR[a + "weight"], Ri, d[i + 1],
-                            d[i + 1], db=GR[a + "bias"], main=True)
-                self._ready_main("D", a)
-                if tail_b:
-                    self._wgrad("D", f"b{i}", D[f"a{i}"], g if self._dbits(i) else D[f"gzb{i}"],
-                                GR[b + "weight"], Ri, d[i + 1], d[i], main=True, **wgb)
-                    self._ready_main("D", b)
+                for _, args, kw, pre in sorted(tail_jobs, key=lambda j: j[0]):
+                    self._wgrad("D", *args, main=True, **kw)
+                    self._ready_main("D", pre)
         if s == 0:
             ops.unpool_mask(D["gh"], D["yrgb"], D["gzrgb"], B=B, H=4, W=4, C=d[0], scale=1.0,
                             slope=SLOPE, ups=False)
