@@ -23,9 +23,10 @@ import time
 # streams must not share a hardware queue (HIP's default is 4 per process): a collective's
 # wait-on-event barrier in a shared queue stalls the compute kernels queued behind it
 # (bench.py --dp-exchange at one rank: -16 % of the step with 4 queues, -4 % with 8 or 16,
-# profiles/r3_dp_queues.txt).  Must be set before the HIP runtime starts.
+# profiles/r3_dp_queues.txt; round 6: -2.0 % with 8, -2.2 % with 16, the plain step itself
+# -0.75 % at 16, profiles/r6_dp_lines.txt).  Must be set before the HIP runtime starts.
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dp-exchange" in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch
 import torch.distributed as dist
@@ -319,6 +320,35 @@ def _engine_opts():
     return engine.engine_options()
 
 
+class _host_breakdown:
+    """PG_BENCH_HOSTLOG: host seconds of a replayed step split into the C++ launch segments
+    and each kind of Python host action between them (the DP exchange's collectives, seals,
+    waits), and the time outside the replay."""
+
+    def __init__(self):
+        from pggan_amd import model as M
+        self.M, self.orig, self.t = M, M._Segments.replay, {}
+        me = self
+
+        def replay(seg):
+            for x in seg.segs:
+                t0 = time.perf_counter()
+                if hasattr(x, "replay"):
+                    x.replay()
+                    k = "cpp segments"
+                else:
+                    x()
+                    f = getattr(x, "func", x)
+                    k = getattr(f, "__name__", "host action")
+                d = me.t.setdefault(k, [0.0, 0])
+                d[0] += time.perf_counter() - t0
+                d[1] += 1
+        M._Segments.replay = replay
+
+    def restore(self):
+        self.M._Segments.replay = self.orig
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -372,11 +402,21 @@ def main():
     # host-side cost of enqueueing one step (kernels are not waited for): if this is close
     # to ms_per_step the step is launch-bound, not GPU-bound.  Measured on the steps the
     # timed loop runs (graph replays in one process), before it.
+    # the first step after a flush starts without a deferred generator update (under DP a
+    # different replay key, whose second occurrence records): one step first, so the two
+    # measured below are the replays the timed loop runs
+    step()
+    hostparts = _host_breakdown() if os.environ.get("PG_BENCH_HOSTLOG") else None
     h0 = time.perf_counter()
     for _ in range(2):
         step()
     model.flush()
     host_ms = (time.perf_counter() - h0) * 1e3 / 2
+    if hostparts is not None:
+        hostparts.restore()
+        log("host enqueue per step (ms): " + ", ".join(
+            f"{k} {v[0] * 1e3 / 2:.3f} ({v[1] / 2:.1f}x)" for k, v in sorted(
+                hostparts.t.items(), key=lambda kv: -kv[1][0])))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -188,7 +188,10 @@ ENGINE_DEFAULTS = dict(
     dbits_min_res=512,     # ... from this resolution; below it the unpool-pass bits (_ubits)
     fuse_ubits=True,
     fuse_rgbbits=True,     # the top fromRGB output's sign bits (see _rgbbits)
-    overlap_g_exchange=True,  # DP: the G all-reduce behind the next step's real-image part
+    # DP: the G all-reduce behind the next step's real-image part (-1: only where the exchange
+    # spans more than one rank -- at one rank (bench.py --dp-exchange) there is no transfer to
+    # hide and the reorder's bookkeeping measured slower, profiles/r6_dp_lines.txt)
+    overlap_g_exchange=-1,
     tail_main=True,        # the last weight gradients of a final pass on the main stream
     sep_b2=True,           # the merged second backward writes its own gradient buffers
     fuse_rgbw=True,        # the final pass's fromRGB weight gradient in the top conv's epilogue
@@ -1617,7 +1620,11 @@ class StepEngine:
         The arithmetic and its order per parameter are the reference's either way."""
         fpG, fpD, hp = self.fpG, self.fpD, self.hyper
         PG, PD = fpG.views, fpD.views
-        if not self.overlap_g_exchange:
+        ov = self.overlap_g_exchange
+        if ov < 0:
+            # a bound GradExchange.hook carries the exchange's world size
+            ov = int(getattr(getattr(grad_hook, "__self__", None), "world", 2) > 1)
+        if not ov:
             self._finish_G()   # the previous step's G exchange completes first (no B2 reorder)
         if self._pending_G is None and not self._packed["G"]:
             self.pack("G", PG)

@@ -14,9 +14,10 @@ import sys
 # streams must not share a hardware queue (HIP's default is 4 per process): a collective's
 # wait-on-event barrier in a shared queue stalls the compute kernels queued behind it
 # (bench.py --dp-exchange at one rank: -16 % of the step with 4 queues, -4 % with 8 or 16,
-# profiles/r3_dp_queues.txt).  Must be set before the HIP runtime starts.
+# profiles/r3_dp_queues.txt; round 6: -2.0 % with 8, -2.2 % with 16, the plain step itself
+# -0.75 % at 16, profiles/r6_dp_lines.txt).  Must be set before the HIP runtime starts.
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--dp-exchange" in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import torch
 
