@@ -142,7 +142,30 @@ class KernelTimer:
             self.shapes.append(("wgrad3x3", kw["H"], kw["cin"], kw["cout"], int(kw["ups"]), a, b,
                                 fl, by))
 
+        def rgb_conv(f):
+            """conv3x3_rgbw / conv3x3_rgbd: the input-gradient conv with the fromRGB backward
+            in its epilogue (no conv output stored; the image read or its gradient written)."""
+            def g(x, wpk, **kw):
+                if not self.on:
+                    return f(x, wpk, **kw)
+                a, b = self.ev(), self.ev()
+                a.record()
+                f(x, wpk, **kw)
+                b.record()
+                fl = 2.0 * kw["B"] * kw["H"] * kw["W"] * 9 * kw["cin"] * kw["cout"]
+                img = kw.get("img") if kw.get("img") is not None else kw.get("gimg")
+                by = (x.numel() * x.element_size() + wpk.numel() * wpk.element_size() +
+                      kw["aux"].numel() * kw["aux"].element_size() +
+                      (img.numel() * img.element_size() if isinstance(img, torch.Tensor) else 0))
+                self.rec["conv3x3"].append((a, b, fl, by))
+                self.shapes.append(("conv3x3", kw["H"], kw["cin"], kw["cout"], kw["flags"], a, b,
+                                    fl, by))
+            return g
+
         ops.conv3x3, ops.conv_wgrad = conv3x3, conv_wgrad
+        if hasattr(ops, "conv3x3_rgbw"):
+            ops.conv3x3_rgbw = rgb_conv(ops.conv3x3_rgbw)
+            ops.conv3x3_rgbd = rgb_conv(ops.conv3x3_rgbd)
 
     def per_shape(self, steps=1):
         agg = {}
@@ -449,7 +472,7 @@ def main():
     # region overlaps weight gradients (side stream) with the input-gradient chain, so its
     # per-launch durations include the other stream's contention; this gives each kernel
     # family's rate in isolation (roofline.isolated)
-    ksum_iso = {}
+    ksum_iso, iso_launches = {}, []
     if timer:
         from pggan_amd import engine as _E
         saved = (timer.rec, timer.shapes)
@@ -462,6 +485,7 @@ def main():
         timer.on = False
         _E.FORCE_SERIAL = False
         ksum_iso = timer.summary()
+        iso_launches = timer._launches()
         if os.environ.get("PG_BENCH_SHAPES"):
             with open(os.environ["PG_BENCH_SHAPES"] + ".iso.json", "w") as f:
                 json.dump(timer.per_shape(1), f, indent=1)
@@ -480,9 +504,13 @@ def main():
         # the instrumented step's conv / wgrad calls in launch order, with the roofline group
         # of each: tools/prof_summary.py aligns them with a --pmc pass's dispatches to give
         # each group its measured HBM bytes per call (roofline.traffic)
-        with open(os.environ["PG_BENCH_LAUNCHES"], "w") as f:
-            json.dump([dict(group=f"{fam}/{bound}", H=H, flops=fl, bytes=by)
-                       for fam, H, fl, by, ms, bound in timer._launches()], f)
+        # (".iso": the one-stream step's calls in ITS order -- the last dispatches of a --pmc
+        # pass; the final pass's tail weight gradients sit elsewhere in the two-stream order)
+        for path, ls in ((os.environ["PG_BENCH_LAUNCHES"], timer._launches()),
+                         (os.environ["PG_BENCH_LAUNCHES"] + ".iso", iso_launches)):
+            with open(path, "w") as f:
+                json.dump([dict(group=f"{fam}/{bound}", H=H, flops=fl, bytes=by)
+                           for fam, H, fl, by, ms, bound in ls], f)
 
     if rank == 0:
         roof = None
