@@ -108,6 +108,13 @@ size_t pg_scratch_bytes(void);
  *                                             s = f / B: gbar = gimg / B)
  * summed over workgroups in a fixed order through `scratch`.  Only through pg_conv3x3_rgbd. */
 #define PG_CONV_RGBD 8192
+/* toRGB output in the epilogue of the generator's top conv b forward (with PG_CONV_PIXNORM:
+ * lib/blocks.py:131-139 then toRGBBlock, lib/blocks.py:153-170, pggan/nets.py:140-156 at
+ * alpha = 1): y (and y2 = the PixelNorm factor) are written as by pg_conv3x3_fwd, and
+ *   img[b][k] = c * (sum_n w_rgb[k][n] y[n] + b_rgb[k])   (fp32 NCHW, y as stored in bf16)
+ * so the top activation is not read back by a separate toRGB pass.  Only through
+ * pg_conv3x3_rgbo. */
+#define PG_CONV_RGBO 16384
 
 typedef struct {
   int B, H, W;     /* conv output spatial size (after the optional input upsample) */
@@ -167,6 +174,13 @@ int pg_conv3x3_rgbw(int dtype, const pg_conv_desc* d, const void* x, const void*
 int pg_conv3x3_rgbd(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
                     const void* aux, const float* w_rgb, float f, float* gimg, float* norms,
                     float* dw, float s, void* scratch, void* stream);
+/* The generator's top conv b forward with PG_CONV_RGBO (d->flags = PIXNORM | LRELU | BIAS |
+ * RGBO): x, wpk, bias, y, y2 as pg_conv3x3_fwd; w_rgb [3][C] / b_rgb [3] the toRGB layer's
+ * weights and bias, c its He constant, img [B][3][H][W] fp32 written.  Replaces pg_conv3x3_fwd
+ * + pg_rgb_out at alpha = 1 (pggan/nets.py:140-156). */
+int pg_conv3x3_rgbo(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const float* bias, void* y, void* y2, const float* w_rgb, const float* b_rgb,
+                    float c, float* img, void* stream);
 /* 1 if pg_conv3x3_fwd supports d->flags for this shape/dtype (the fused epilogues depend
  * on the tile the dispatcher picks), 0 otherwise.  ws_bytes as passed to the launch. */
 int pg_conv3x3_supported(int dtype, const pg_conv_desc* d, size_t ws_bytes);

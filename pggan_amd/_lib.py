@@ -20,6 +20,7 @@ CONV_PIXNORM = 64
 CONV_PNBWD = 2048
 CONV_RGBW = 4096
 CONV_RGBD = 8192
+CONV_RGBO = 16384
 CONV_Y2_BITS, CONV_AUX_BITS, CONV_X_BITS, CONV_GZ_BITS = 128, 256, 512, 1024
 PACK_FWD, PACK_DGRAD = 0, 1
 LIN_BIAS, LIN_LRELU, LIN_MASK, LIN_IN_CHW, LIN_OUT_CHW, LIN_F32_IN, LIN_F32_OUT = (
@@ -102,6 +103,8 @@ _SIGS = {
                         _I),
     "pg_conv3x3_rgbd": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _F, _VP, _VP, _VP, _F,
                          _VP, _VP], _I),
+    "pg_conv3x3_rgbo": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _F, _VP,
+                         _VP], _I),
     "pg_conv3x3_fwd_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP,
                            _SZ, _VP], _I),
     "pg_conv3x3_wgrad_ex": ([_I, ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _F, _VP, _VP, _VP, _SZ,
@@ -425,6 +428,19 @@ class HipOps:
                                            _p(img), float(s), _p(dw), _p(db),
                                            self._scr(), self._s()),
                   "conv3x3_rgbw")
+
+    def conv3x3_rgbo(self, x, wpk, y, *, B, H, W, cin, cout, flags, bias, w_rgb, b_rgb, c, img,
+                     y2=None, slope=0.2):
+        """The generator's top conv b forward with PixelNorm (flags PIXNORM | LRELU | BIAS) and
+        the toRGB output img = c (W_rgb y + b_rgb) of its stored y in the epilogue
+        (include/pggan_hip.h: PG_CONV_RGBO); y and y2 as conv3x3."""
+        self._cuda(x, wpk, y, bias, y2, w_rgb, b_rgb, img)
+        d = ConvDesc(B, H, W, cin, cout, x.shape[-1], y.shape[-1], 0,
+                     y2.shape[-1] if y2 is not None else 0, flags | CONV_RGBO, slope, 1.0, 0)
+        self._chk(self.lib.pg_conv3x3_rgbo(self._dt(y), ctypes.byref(d), _p(x), _p(wpk), _p(bias),
+                                           _p(y), _p(y2), _p(w_rgb), _p(b_rgb), float(c), _p(img),
+                                           self._s()),
+                  "conv3x3_rgbo")
 
     def conv3x3_rgbd(self, x, wpk, *, B, H, W, cin, cout, flags, aux, w_rgb, f, gimg,
                      norms=None, dw=None, s=0.0, slope=0.2, out_scale=1.0):

@@ -61,6 +61,9 @@ struct ConvParams {
   float* gimg;        // fp32 NCHW [B][3][H][W], written
   float* norms;       // [B] per-sample squared norms, accumulated (or NULL)
   float f2;           // gimg = f2 * W^T gz
+  // PG_CONV_RGBO: the toRGB output of the conv result (rw = toRGB weights [3][cout], gimg = the
+  // image written, f2 = its He constant)
+  const float* rb;    // toRGB bias [3]
 };
 
 // the RGBW operands of the next conv_hr launch on this host thread (pg_conv3x3_rgbw)
@@ -75,6 +78,8 @@ struct RgbwArgs {
   float* gimg = nullptr;
   float* norms = nullptr;
   float f = 0.f;
+  // RGBO (rw, gimg, f as above)
+  const float* rb = nullptr;
 };
 static thread_local RgbwArgs g_rgbw;
 
@@ -1714,6 +1719,13 @@ int launch_tr(const pg_conv_desc* d, const void* x, const void* wpk, const float
 template <typename T>
 bool conv_supported(const pg_conv_desc* d, size_t wsb) {
   constexpr int BITS = PG_CONV_Y2_BITS | PG_CONV_AUX_BITS | PG_CONV_X_BITS;
+  if (d->flags & PG_CONV_RGBO) {   // the EF tiles 0 / 5 (16 / 32 channels), PixelNorm forward
+    if constexpr (sizeof(T) != 2) return false;
+    constexpr int PN = PG_CONV_PIXNORM | PG_CONV_LRELU | PG_CONV_BIAS;
+    if (d->flags != (PN | PG_CONV_RGBO) || !conv_hr_ok(d)) return false;
+    const int t = conv_hr_tile(d);
+    return (t == 0 && d->cout == 16) || (t == 5 && d->cout == 32);
+  }
   if (d->flags & (PG_CONV_RGBW | PG_CONV_RGBD)) {   // the EF tiles 0 / 5 (16 / 32 channels)
     if constexpr (sizeof(T) != 2) return false;
     const int rf = d->flags & (PG_CONV_RGBW | PG_CONV_RGBD);
@@ -1913,6 +1925,23 @@ int pg_conv3x3_rgbd(int dtype, const pg_conv_desc* d, const void* x, const void*
   g_rgbw.rw = w_rgb; g_rgbw.f = f; g_rgbw.gimg = gimg; g_rgbw.norms = norms; g_rgbw.dw = dw;
   g_rgbw.s = s; g_rgbw.scratch = (float*)scratch;
   const int rc = conv_dispatch<bf16_t>(d, x, wpk, nullptr, aux, nullptr, nullptr, nullptr, 0,
+                                       (hipStream_t)stream);
+  g_rgbw = RgbwArgs{};
+  return rc;
+}
+
+int pg_conv3x3_rgbo(int dtype, const pg_conv_desc* d, const void* x, const void* wpk,
+                    const float* bias, void* y, void* y2, const float* w_rgb, const float* b_rgb,
+                    float c, float* img, void* stream) {
+  PG_CHECK_ARG(d && x && wpk && bias && y && w_rgb && b_rgb && img, "conv3x3_rgbo: null pointer");
+  PG_CHECK_ARG(dtype == PG_BF16 && (d->flags & PG_CONV_RGBO) && conv_supported<bf16_t>(d, 0),
+               "conv3x3_rgbo: flags 0x%x not supported for %d -> %d at %dx%d", d->flags, d->cin,
+               d->cout, d->H, d->W);
+  PG_CHECK_ARG(d->x_cs >= cinp_of(d->cin) && d->x_cs % 8 == 0 && d->y_cs >= d->cout,
+               "conv3x3_rgbo: bad channel strides");
+  g_rgbw = RgbwArgs{};
+  g_rgbw.rw = w_rgb; g_rgbw.rb = b_rgb; g_rgbw.f = c; g_rgbw.gimg = img;
+  const int rc = conv_dispatch<bf16_t>(d, x, wpk, bias, nullptr, y, y2, nullptr, 0,
                                        (hipStream_t)stream);
   g_rgbw = RgbwArgs{};
   return rc;

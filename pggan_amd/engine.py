@@ -199,6 +199,7 @@ ENGINE_DEFAULTS = dict(
     fuse_torgb_wg=True,    # the toRGB weight gradient in the toRGB input-gradient pass
     tail_b=True,           # ... with tail_main: the top level's conv-b weight gradient too
     tail_levels=1,         # ... and both weight gradients of this many top levels
+    fuse_rgbo=False,       # the toRGB output in the epilogue of the top conv b: measured -1 % (opt-in)
 )
 
 
@@ -832,17 +833,47 @@ class StepEngine:
         self._g_conv_pn("first", g["h0"], g["u0"], g["y0"], g["r0"], 4, d[0], d[0], L.CONV_LRELU,
                         keep)                                                # blocks.py:131-139
         prev = g["y0"]
+        rgbo = s >= 1 and not self._low(alpha) and self._rgbo()
         for i in range(s):                                                   # nets.py:144-149
             Ri = 8 * 2 ** i
             self._g_conv_pn(f"a{i}", prev, g[f"ua{i}"], g[f"ya{i}"], g[f"ra{i}"], Ri, d[i],
                             d[i + 1], L.CONV_UPS_IN | L.CONV_LRELU, keep)
-            self._g_conv_pn(f"b{i}", g[f"ya{i}"], g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], Ri,
-                            d[i + 1], d[i + 1], L.CONV_LRELU, keep)
+            if i == s - 1 and rgbo:
+                # the top conv b with the toRGB output in its epilogue (PG_CONV_RGBO: the top
+                # activation is not read back by a separate toRGB pass)
+                pf, _, bs, _ = self.packs[("G", f"b{i}")]
+                pre = f"toRGB_blocks.{s}.toRGB.module."
+                ops.conv3x3_rgbo(g[f"ya{i}"], pf, g[f"yb{i}"], B=B, H=Ri, W=Ri, cin=d[i + 1],
+                                 cout=d[i + 1], flags=L.CONV_PIXNORM | L.CONV_LRELU | L.CONV_BIAS,
+                                 bias=bs, y2=g[f"rb{i}"] if keep else None,
+                                 w_rgb=P[pre + "weight"], b_rgb=P[pre + "bias"], c=he(d[s]),
+                                 img=g["img"], slope=SLOPE)                   # nets.py:140-156
+            else:
+                self._g_conv_pn(f"b{i}", g[f"ya{i}"], g[f"ub{i}"], g[f"yb{i}"], g[f"rb{i}"], Ri,
+                                d[i + 1], d[i + 1], L.CONV_LRELU, keep)
             prev = g[f"yb{i}"]
-        self._rgb_out(P, alpha)
+        if not rgbo:
+            self._rgb_out(P, alpha)
         if self.trace is not None:
             self.trace("G", self)
         return g["img"]
+
+    def _rgbo(self):
+        """Whether the top conv b can write the toRGB output in its epilogue (PG_CONV_RGBO): the
+        fused PixelNorm forward on a tile holding every channel, at every batch the G forward
+        runs (B, and 2B merged)."""
+        if "rgbo" not in self._ws_cache:
+            s, d = self.s, self.depths
+            f = getattr(self.ops, "conv_supported", None)
+            ok = bool(self.fuse_rgbo and self.fuse_pixnorm and f is not None and
+                      hasattr(self.ops, "conv3x3_rgbo") and
+                      self._pn_fused(self.R, d[s], d[s], L.CONV_LRELU))
+            if ok:
+                flags = L.CONV_PIXNORM | L.CONV_LRELU | L.CONV_BIAS | L.CONV_RGBO
+                ok = all(f(B=b, H=self.R, W=self.R, cin=d[s], cout=d[s], flags=flags, ws_bytes=0)
+                         for b in (self.B, 2 * self.B))
+            self._ws_cache["rgbo"] = ok
+        return self._ws_cache["rgbo"]
 
     def _ylvl(self, j):
         return self.g["y0"] if j == 0 else self.g[f"yb{j - 1}"]

@@ -1034,3 +1034,44 @@ def test_conv_rgbd_epilogue(B, H, C):
                            (outs[0][2].view(C, 3), dw_ref, "dw")):
         err = float((got.double() - ref).norm() / ref.norm())
         assert err <= 1e-4, (what, err)
+
+
+@pytest.mark.parametrize("B,H,C,keep", [(4, 1024, 16, True), (8, 1024, 16, False), (2, 512, 32, True)])
+def test_conv_rgbo_epilogue(B, H, C, keep):
+    """PG_CONV_RGBO (bf16): the generator's top conv b forward with PixelNorm and the toRGB output
+    img = c (W y + b) in its epilogue, against the unfused pair (the same conv, then
+    pg_rgb_out on the stored y): y and the PixelNorm factor bitwise equal, img within fp32
+    summation-order rounding (1e-5 relative L2; the epilogue sums the 16 / 32 channels as
+    per-lane partials, the toRGB pass in channel order)."""
+    from cpu_ops import CONV_BIAS, CONV_LRELU, CONV_PIXNORM
+    hip, _ = ops_pair(torch.bfloat16)
+    fl = CONV_PIXNORM | CONV_LRELU | CONV_BIAS
+    assert hip.conv_supported(B=B, H=H, W=H, cin=C, cout=C, flags=fl | _lib_flag("CONV_RGBO"))
+    dt = torch.bfloat16
+    x = q(rnd(B, H, H, C, seed=141), dt).to(dt).cuda()
+    w = rnd(C, C, 3, 3, seed=142)
+    scale = 1.0 / (9 * C) ** 0.5
+    wp = torch.zeros(hip.packed_elems(0, C, C), dtype=dt, device="cuda")
+    hip.conv_pack(0, w.cuda(), scale, wp)
+    bias = (rnd(C, seed=143) * 0.1 * scale).cuda()
+    w_rgb, b_rgb = rnd(3, C, seed=144).cuda(), (rnd(3, seed=145) * 0.1).cuda()
+    c = (1.0 / C) ** 0.5
+    outs = []
+    for fused in (True, False):
+        y = torch.zeros(B, H, H, C, dtype=dt, device="cuda")
+        r = torch.zeros(B, H, H, dtype=torch.float32, device="cuda") if keep else None
+        img = torch.zeros(B, 3, H, H, dtype=torch.float32, device="cuda")
+        if fused:
+            hip.conv3x3_rgbo(x, wp, y, B=B, H=H, W=H, cin=C, cout=C, flags=fl, bias=bias, y2=r,
+                             w_rgb=w_rgb, b_rgb=b_rgb, c=c, img=img)
+        else:
+            hip.conv3x3(x, wp, y, B=B, H=H, W=H, cin=C, cout=C, flags=fl, bias=bias, y2=r)
+            hip.rgb_out(y, w_rgb, b_rgb, c, img, B=B, R=H, C=C)
+        torch.cuda.synchronize()
+        outs.append((y.cpu(), None if r is None else r.cpu(), img.cpu()))
+    (yf, rf, imf), (yu, ru, imu) = outs
+    assert torch.equal(yf, yu), "fused y differs"
+    if keep:
+        assert torch.equal(rf, ru), "fused PixelNorm factor differs"
+    err = float((imf.double() - imu.double()).norm() / imu.double().norm())
+    assert err <= 1e-5, err
