@@ -130,12 +130,20 @@ struct Frag<float> {
   }
 };
 
+// waves along M of the 64-output-channel compile-time tiles (the 16^2 / 32^2 split-K convs):
+// 2 -> four waves of 64 x 32 outputs, 4 -> eight waves of 32 x 32 (half the accumulators and
+// staging registers per wave, two waves per SIMD): 16^2 512 -> 512 20.7 -> 19.1 us per launch
+// at B = 4, 27.6 -> 25.2 at B = 8, step 10.084 -> 10.030 ms (profiles/r6_c64_waves_ab.txt)
+#ifndef PG_C64_WM
+#define PG_C64_WM 4
+#endif
+
 // CKC > 0: the channel chunk is fixed at compile time (CKC == p.CK), so the k-step loop
 // unrolls and each k-step's tap / channel offset is a constant (the 4x4..64x64 convs at
 // 256-512 channels are otherwise bound by that per-k-step index arithmetic)
 template <typename T, int BM, int BN, int WM, int WN, int MAXV, bool TR, int CKC = 0, int TWC = 0,
           int THC = 0>
-__global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(ConvParams p) {
   // geometry: compile-time where the launch fixes it (TWC/THC/CKC > 0), else from p
   constexpr int SZ = (int)sizeof(T);
   const int cTW = TWC > 0 ? TWC : p.TW, cTH = THC > 0 ? THC : p.TH;
@@ -147,7 +155,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const int chalo = (CKC > 0 && TWC > 0) ? ((cNB * (cTH + 2) * (cTW + 2) * cpixb + 15) & ~15) : p.halo_bytes;
   constexpr int MT = BM / WM / 16;
   constexpr int NT = BN / WN / 16;
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 waves");
+  constexpr int NTHR = 64 * WM * WN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -210,7 +219,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   const int ntot = nhv + BN * ntap_pad * vpp;
 #pragma unroll
   for (int j = 0; j < MAXV; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTHR * j;
     soff[j] = -1;
     loff[j] = -1;
     if (i < nhv) {
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
   T* y = reinterpret_cast<T*>(p.y);
   if (p.ws) {   // split-K partial: raw fp32 sums to this split's slab, [pixel][cout_p]
     float* slab = p.ws + bz * p.slab;
-    for (int i = tid; i < BM * NV; i += 256) {
+    for (int i = tid; i < BM * NV; i += NTHR) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
       if (n >= p.cout_p) continue;
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
           *reinterpret_cast<const f32x4_t*>(ot + pm * ORS + cv);
     }
   } else if (!(p.flags & PG_CONV_POOL)) {
-    for (int i = tid; i < BM * NV; i += 256) {
+    for (int i = tid; i < BM * NV; i += NTHR) {
       const int pm = i / NV, cv = (i - pm * NV) * 4;
       const int n = n0 + cv;
       if (n >= p.cout) continue;
@@ -499,7 +508,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvParams p) {
     const int PTW = cTW >> 1, PTH = cTH >> 1;
     const int Ho = p.H >> 1, Wo = p.W >> 1;
     T* y2 = reinterpret_cast<T*>(p.y2);
-    for (int i = tid; i < (BM / 4) * NV; i += 256) {
+    for (int i = tid; i < (BM / 4) * NV; i += NTHR) {
       const int pp = i / NV, cv = (i - pp * NV) * 4;
       const int n = n0 + cv;
       if (n >= p.cout) continue;
@@ -1657,8 +1666,8 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   {
     const int vpp = p.CK * (int)sizeof(T) / 16;
     const int ntot = tc.NB * (tc.TH + 2) * (tc.TW + 2) * vpp + BN * (p.KS * 32 / p.CK) * vpp;
-    PG_CHECK_ARG(ntot <= 256 * MAXV, "conv3x3: %d staged vectors exceed %d per block", ntot,
-                 256 * MAXV);
+    PG_CHECK_ARG(ntot <= 64 * WM * WN * MAXV, "conv3x3: %d staged vectors exceed %d per block", ntot,
+                 64 * WM * WN * MAXV);
     (void)0;
   }
   int splits = 1;
@@ -1671,7 +1680,8 @@ int launch_conv(const pg_conv_desc* d, const void* x, const void* wpk, const flo
   dim3 grid(pg_cdiv(d->B, tc.NB) * p.tiles_x * p.tiles_y, p.cout_p / BN + (p.cout_p % BN ? 1 : 0),
             splits);
   PG_LDS_ATTR((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), 160 * 1024);
-  PG_KLAUNCH((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(256), lds, st, p);
+  PG_KLAUNCH((conv3x3_kernel<T, BM, BN, WM, WN, MAXV, TR, CKC, TWC, THC>), grid, dim3(64 * WM * WN), lds,
+             st, p);
   if (splits > 1) {
     const bool pool = (d->flags & PG_CONV_POOL) != 0;
     const size_t n = (size_t)d->B * (pool ? d->H / 2 : d->H) * (pool ? d->W / 2 : d->W) * (d->cout / 4);
@@ -1786,7 +1796,7 @@ int conv_dispatch(const pg_conv_desc* d, const void* x, const void* wpk, const f
         const TileCfg tc = pick_tile(d->H, d->W, 128, 64);
 #define PG_LC(tw, th)                                                                            \
   if (tc.TW == tw && tc.TH == th)                                                                \
-    return launch_conv<T, 128, 64, 2, 2, 16, false, 32, tw, th>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
+    return launch_conv<T, 128, 64, PG_C64_WM, 2, 16 * 2 / PG_C64_WM, false, 32, tw, th>(d, x, wpk, bias, aux, y, y2, ws, wsb, st);
         PG_LC(4, 4)
         PG_LC(8, 8)
         PG_LC(16, 8)
