@@ -1,17 +1,13 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-ROOT=$(pwd); export TMPDIR=/tmp
-timeout -k 10 120 python tools/glue_bench.py --iters 1 --check ab/lib_unpoolv.so || exit 1
-for v in new=pggan_amd/libpggan_hip.so old=ab/lib_unpoolv.so; do
-  name=${v%%=*}; lib=${v#*=}; rm -rf gpurun_out/gb_$name
-  ( cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/gb_$name" -o run -- python "$ROOT/tools/glue_bench.py" --lib "$ROOT/$lib" ) > gpurun_out/gb_$name.log 2>&1 || { echo "$name failed"; exit 1; }
-done
-for n in new old; do echo "== $n"; python - <<PY
-import csv,collections
-d=collections.defaultdict(list)
-for r in csv.DictReader(open('gpurun_out/gb_$n/run_kernel_trace.csv')):
-    k=r['Kernel_Name']
-    if 'unpool' in k: d[(k.split('(')[0][-30:],r['Grid_Size_X'],r['Grid_Size_Y'])].append((int(r['End_Timestamp'])-int(r['Start_Timestamp']))/1e3)
-for k,v in d.items(): v.sort(); print(k, len(v), 'med', v[len(v)//2])
-PY
-done
+( while sleep 50; do date +%T >> gpurun_out/heartbeat.log; done ) & hb=$!
+timeout -k 10 1100 python -u -m pytest tests -v -m gpu --ignore=tests/test_gpu_baseline_parity.py --ignore=tests/test_gpu_dp.py --timeout 600 --timeout-method thread > gpurun_out/gpuA.log 2>&1; rc=$?
+echo "gpuA rc=$rc"; tail -n 2 gpurun_out/gpuA.log
+[ $rc -eq 0 ] || { kill $hb; exit $rc; }
+PG_PARITY_OUT=gpurun_out/parity_r6v5 timeout -k 10 600 python -u -m pytest tests/test_gpu_baseline_parity.py -v -m gpu -k bf16 --timeout 500 --timeout-method thread -s > gpurun_out/gpuC5.log 2>&1; rc=$?
+echo "gpuC5 rc=$rc"; tail -n 2 gpurun_out/gpuC5.log
+[ $rc -eq 0 ] || { kill $hb; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -n 1 gpurun_out/smoke.log
+kill $hb
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -n 1 gpurun_out/bench.log | cut -c1-300
